@@ -1,0 +1,175 @@
+"""ctypes binding of libbigcodec_hip.so (the C ABI declared in include/bigcodec.h).
+
+The HIP library IS the compute path: there is no eager-PyTorch or CPU fallback.  If the library is
+missing or fails to load, every op raises immediately (BigCodecLibraryError).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbigcodec_hip.so")
+_lock = threading.Lock()
+_lib = None
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_longlong
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "bc_abi_version": (I, []),
+    "bc_conv1d_select_cfg": (I, [I, I]),
+    "bc_conv1d_packed_floats": (L, [I, I, I, I]),
+    "bc_conv1d_pack": (I, [P, P, I, I, I, I]),
+    "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "bc_convT1d_phase_taps": (I, [I, I]),
+    "bc_convT1d_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
+    "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
+    "bc_aa_snake_fwd": (I, [P, P, P, P, P, P, I, I, I, P]),
+    "bc_lstm_hh_packed_floats": (L, [I]),
+    "bc_lstm_pack_hh": (I, [P, P, I]),
+    "bc_lstm_workspace_floats": (L, [I, I, I]),
+    "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P]),
+    "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
+    "bc_vq_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P]),
+    "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
+    "bc_vq2emb": (I, [P, L, P, P, P, P, L, I, I, I, I, P]),
+    "bc_rvq_update": (I, [P, P, P, L, I, P]),
+    "bc_btc_to_ctb": (I, [P, P, I, I, I, P]),
+    "bc_ctb_to_btc_add": (I, [P, P, P, I, I, I, P]),
+    "bc_synth_clips": (I, [P, I, L, L, P]),
+}
+EXPORTED = tuple(_SIGS)
+
+_ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
+
+
+class BigCodecLibraryError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes CDLL with argtypes set."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or _LIB_PATH
+        if not os.path.exists(p):
+            raise BigCodecLibraryError(
+                f"{p} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()' "
+                f"or python audiotokenization_amd/build_lib.py). There is no CPU/eager fallback.")
+        try:
+            lib = C.CDLL(p)
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise BigCodecLibraryError(f"failed to load {p}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise BigCodecLibraryError(f"{name} failed: {_ERR.get(rc, rc)} (code {rc})")
+
+
+def call(name: str, *args) -> int:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device (or host numpy) pointer of a tensor/array; None stays NULL."""
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def stream_of(t) -> int | None:
+    import torch
+
+    if not t.is_cuda:
+        raise BigCodecLibraryError("BigCodec HIP ops take device tensors (got a CPU tensor)")
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class KernelTimer:
+    """Per-launch HIP-event timing of selected library calls (used by bench.py inside its timed
+    region).  Events are recorded on the stream the kernel is launched on (torch's current stream,
+    the one every op here passes to the library)."""
+
+    def __init__(self):
+        self.records = []  # (kernel symbol, flops, bytes, ev_start, ev_end)
+
+    def begin(self):
+        import torch
+
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, ev0, kernel: str, flops: float, nbytes: float):
+        import torch
+
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.append((kernel, flops, nbytes, ev0, ev1))
+
+    def summary(self):
+        """{kernel: dict(launches, ms_total, flops_total, bytes_total)} (synchronises)."""
+        import torch
+
+        torch.cuda.synchronize()
+        out = {}
+        for k, fl, nb, e0, e1 in self.records:
+            d = out.setdefault(k, dict(launches=0, ms_total=0.0, flops_total=0.0, bytes_total=0.0))
+            d["launches"] += 1
+            d["ms_total"] += e0.elapsed_time(e1)
+            d["flops_total"] += fl
+            d["bytes_total"] += nb
+        return out
+
+
+_timer: KernelTimer | None = None
+
+
+def set_timer(t: KernelTimer | None) -> None:
+    global _timer
+    _timer = t
+
+
+def active_timer() -> KernelTimer | None:
+    return _timer
+
+
+# conv tile configs (csrc/conv1d.hip kCfgs) -> template arguments, for kernel-symbol naming
+CONV_CFGS = {0: (4, 2, 4, 2, 8), 1: (4, 1, 4, 4, 8), 2: (3, 1, 4, 4, 8), 3: (2, 1, 4, 4, 8), 4: (1, 1, 4, 4, 8),
+             5: (4, 2, 4, 2, 4), 6: (4, 1, 4, 4, 4), 7: (3, 1, 4, 4, 4), 8: (2, 1, 4, 4, 4), 9: (1, 1, 4, 4, 4)}
+
+
+def conv_kernel_name(cfg: int, snake: bool) -> str:
+    mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
+    return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}, {'true' if snake else 'false'}>"
+
+
+def ptr_array(ptrs):
+    arr = (C.c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr

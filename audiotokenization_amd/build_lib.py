@@ -1,0 +1,82 @@
+"""Build libbigcodec_hip.so (gfx950) in-tree with hipcc.
+
+The shared library is the product: every compute kernel of the BigCodec path lives in
+audiotokenization_amd/csrc/*.hip and is exported through the C ABI in include/bigcodec.h.
+Built objects stay in-tree (git-ignored) so they travel with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD = os.path.join(PKG_DIR, "_build")
+LIB = os.path.join(PKG_DIR, "libbigcodec_hip.so")
+ARCH = os.environ.get("BIGCODEC_ARCH", "gfx950")
+
+SOURCES = ["conv1d.hip", "elementwise.hip", "lstm.hip", "vq.hip", "abi.hip"]
+HEADERS = ["bc_common.h", "bc_internal.h"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the BigCodec HIP library cannot be built")
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(REPO, "include", "bigcodec.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile (if sources changed) and return the path of libbigcodec_hip.so."""
+    os.makedirs(BUILD, exist_ok=True)
+    stamp = os.path.join(BUILD, "stamp")
+    dig = _digest()
+    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+        with open(stamp) as fh:
+            if fh.read().strip() == dig:
+                return LIB
+    hipcc = _hipcc()
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(BUILD, src.replace(".hip", ".o"))
+        cmd = [hipcc, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{res.stderr}")
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{res.stderr}")
+    os.replace(tmp, LIB)
+    with open(stamp, "w") as fh:
+        fh.write(dig)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,138 @@
+"""BigCodecEncoder / BigCodecDecoder (vq/codec_encoder.py:14-90, vq/codec_decoder.py:15-142) on the
+HIP kernels, with the reference's constructor signatures, state_dict keys and call surface."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .modules import (Activation1d, DecoderBlock, EncoderBlock, ResidualVQ, ResLSTM, SnakeBeta, WNConv1d,
+                      _as_input, run_activation_then)
+
+
+class _Tanh(nn.Module):
+    """nn.Tanh position holder in the decoder Sequential; the tanh is fused into the last conv's
+    epilogue (bc_conv1d_fwd epilogue=1) when the decoder runs as a whole."""
+
+    def forward(self, x):  # standalone use of decoder.model[-1] is not a hot path
+        raise NotImplementedError("the decoder's final tanh runs fused in the last conv")
+
+
+class BigCodecEncoder(nn.Module):
+    """vq/codec_encoder.py:14-90.  forward(x (B,1,T) f32 device) -> (B, out_channels, T/hop)."""
+
+    def __init__(self, ngf=48, use_rnn=True, rnn_bidirectional=False, causal=False, antialias=False,
+                 rnn_num_layers=2, up_ratios=(2, 2, 2, 5, 5), dilations=(1, 3, 9), out_channels=1024):
+        super().__init__()
+        self.hop_length = np.prod(up_ratios)
+        self.ngf = ngf
+        self.up_ratios = up_ratios
+        if causal:
+            assert not rnn_bidirectional
+        d_model = ngf
+        block = [WNConv1d(1, d_model, kernel_size=7, padding=3, causal=causal)]
+        for stride in up_ratios:
+            d_model *= 2
+            block += [EncoderBlock(d_model, stride=stride, dilations=dilations, causal=causal, antialias=antialias)]
+        if use_rnn:
+            block += [ResLSTM(d_model, num_layers=rnn_num_layers, bidirectional=rnn_bidirectional)]
+        block += [
+            Activation1d(activation=SnakeBeta(d_model, alpha_logscale=True), antialias=antialias),
+            WNConv1d(d_model, out_channels, kernel_size=3, padding=1, causal=causal),
+        ]
+        self.block = nn.Sequential(*block)
+        self.enc_dim = d_model
+
+    def forward(self, x):
+        x = _as_input(x)
+        blk = self.block
+        n = len(blk)
+        for i in range(n - 2):
+            x = blk[i](x)
+        h, co = run_activation_then(blk[n - 2], x)
+        return blk[n - 1].run(h, snake=co)
+
+    def inference(self, x):
+        return self.forward(x)
+
+    def remove_weight_norm(self):
+        for m in self.modules():
+            if hasattr(m, "remove_weight_norm") and m is not self and "weight_v" in m._parameters:
+                m.remove_weight_norm()
+
+
+class BigCodecDecoder(nn.Module):
+    """vq/codec_decoder.py:15-142.  forward(x, vq=True) -> (z_q, codes (Nq,B,F), losses (Nq,));
+    forward(x, vq=False) -> waveform (B, 1, T)."""
+
+    def __init__(self, in_channels=1024, upsample_initial_channel=1536, ngf=48, use_rnn=True,
+                 rnn_bidirectional=False, rnn_num_layers=2, up_ratios=(5, 5, 2, 2, 2), dilations=(1, 3, 9),
+                 causal=False, antialias=False, fsq=False, fsq_levels=[4, 4, 4, 8], vq_num_quantizers=1,
+                 vq_commit_weight=0.25, vq_weight_init=False, vq_full_commit_loss=False, codebook_size=8192,
+                 codebook_dim=8):
+        super().__init__()
+        self.hop_length = np.prod(up_ratios)
+        self.ngf = ngf
+        self.up_ratios = up_ratios
+        self.fsq = fsq
+        if fsq:
+            raise NotImplementedError("FSQ quantizer (fsq=True) is a SURVEY §8(f) 'next' item; no shipped "
+                                      "config enables it")
+        self.quantizer = ResidualVQ(num_quantizers=vq_num_quantizers, dim=in_channels,
+                                    codebook_size=codebook_size, codebook_dim=codebook_dim,
+                                    threshold_ema_dead_code=2, commitment=vq_commit_weight,
+                                    weight_init=vq_weight_init, full_commit_loss=vq_full_commit_loss)
+        channels = upsample_initial_channel
+        layers = [WNConv1d(in_channels, channels, kernel_size=7, padding=3, causal=causal)]
+        if use_rnn:
+            layers += [ResLSTM(channels, num_layers=rnn_num_layers, bidirectional=rnn_bidirectional)]
+        output_dim = channels
+        for i, stride in enumerate(up_ratios):
+            input_dim = channels // 2 ** i
+            output_dim = channels // 2 ** (i + 1)
+            layers += [DecoderBlock(input_dim, output_dim, stride, dilations, causal=causal, antialias=antialias)]
+        layers += [
+            Activation1d(activation=SnakeBeta(output_dim, alpha_logscale=True), antialias=antialias),
+            WNConv1d(output_dim, 1, kernel_size=7, padding=3, causal=causal),
+            _Tanh(),
+        ]
+        self.model = nn.Sequential(*layers)
+
+    def decode(self, x):
+        """self.model(x) with the final Snake and tanh fused into the last conv."""
+        x = _as_input(x)
+        m = self.model
+        n = len(m)
+        for i in range(n - 3):
+            x = m[i](x)
+        h, co = run_activation_then(m[n - 3], x)
+        return m[n - 2].run(h, snake=co, epilogue=1)
+
+    def forward(self, x, vq=True):
+        if vq is True:
+            return self.quantizer(x)
+        return self.decode(x)
+
+    def vq2emb(self, vq):
+        self.quantizer = self.quantizer.eval()
+        return self.quantizer.vq2emb(vq)
+
+    def get_emb(self):
+        self.quantizer = self.quantizer.eval()
+        return self.quantizer.get_emb()
+
+    def inference_vq(self, vq):
+        return self.decode(vq[None, :, :])
+
+    def inference_0(self, x):
+        x, q, loss = self.quantizer(x)
+        return self.decode(x), None
+
+    def inference(self, x):
+        return self.decode(x), None
+
+    def remove_weight_norm(self):
+        for m in self.modules():
+            if hasattr(m, "remove_weight_norm") and m is not self and "weight_v" in m._parameters:
+                m.remove_weight_norm()

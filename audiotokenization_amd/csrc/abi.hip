@@ -1,0 +1,228 @@
+// extern "C" entry points of libbigcodec_hip.so (declared and documented in include/bigcodec.h).
+#include "../../include/bigcodec.h"
+#include "bc_common.h"
+#include "bc_internal.h"
+
+using namespace bc;
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+extern "C" {
+
+int bc_abi_version(void) { return BC_ABI_VERSION; }
+
+int bc_conv1d_select_cfg(int Cout, int Cin) {
+  if (Cout <= 0 || Cin <= 0) return -1;
+  return conv_select_cfg(Cout, Cin);
+}
+
+long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg) {
+  if (Cout <= 0 || Cin <= 0 || K <= 0 || cfg < 0 || cfg > 9) return -1;
+  return conv_packed_floats(Cout, Cin, K, cfg);
+}
+
+int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg) {
+  if (!w_host || !packed_host || Cout <= 0 || Cin <= 0 || K <= 0 || cfg < 0 || cfg > 9)
+    return BC_ERR_ARG;
+  conv_pack_weight(w_host, packed_host, Cout, Cin, K, cfg);
+  return BC_OK;
+}
+
+int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias,
+                  const float* snake_alpha_exp, const float* snake_inv_beta, const float* residual,
+                  float* y, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+                  int dilation, int pad_left, int epilogue, int cfg, void* stream) {
+  if (!x || !w_packed || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 ||
+      stride <= 0 || dilation <= 0 || pad_left < 0 || cfg < 0 || cfg > 9)
+    return BC_ERR_ARG;
+  if ((snake_alpha_exp == nullptr) != (snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (epilogue != 0 && epilogue != 1) return BC_ERR_ARG;
+  if (cfg != conv_select_cfg(Cout, Cin)) return BC_ERR_ARG;
+  if (B == 0 || Tout == 0) return BC_OK;
+  ConvArgs a{};
+  a.x = x; a.w = w_packed; a.bias = bias; a.sa = snake_alpha_exp; a.sb = snake_inv_beta;
+  a.res = residual; a.y = y;
+  a.xbs = (long long)Cin * Tin; a.ybs = (long long)Cout * Tout; a.rbs = a.ybs;
+  a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = Tout;
+  a.K = K; a.s = stride; a.d = dilation; a.pl = pad_left;
+  a.yT = Tout; a.ostride = 1; a.ooff = 0; a.epi = epilogue;
+  return conv_launch(a, B, cfg, S(stream));
+}
+
+int bc_convT1d_phase_taps(int K, int stride) {
+  if (K <= 0 || stride <= 0) return -1;
+  return (K + stride - 1) / stride;
+}
+
+int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bias,
+                   const float* snake_alpha_exp, const float* snake_inv_beta, float* y, int B,
+                   int Cin, int Tin, int Cout, int Tout, int K, int stride, int padding, int cfg,
+                   void* stream) {
+  if (!x || !w_phases || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 ||
+      stride <= 0 || padding < 0 || cfg < 0 || cfg > 9)
+    return BC_ERR_ARG;
+  if ((snake_alpha_exp == nullptr) != (snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (cfg != conv_select_cfg(Cout, Cin)) return BC_ERR_ARG;
+  if (B == 0 || Tout == 0) return BC_OK;
+  const int s = stride, p = padding;
+  const int Kp = (K + s - 1) / s;  // taps per phase
+  for (int r = 0; r < s; ++r) {
+    if (!w_phases[r]) return BC_ERR_ARG;
+    // outputs t = s*q - p + r, q in [q_lo, q_hi]
+    const int q_lo = (p - r + s - 1 >= 0) ? (p - r + s - 1) / s : -((r - p) / s);
+    const long long q_hi_num = (long long)Tout - 1 + p - r;
+    const int q_hi = q_hi_num >= 0 ? (int)(q_hi_num / s) : -1;
+    const int nout = q_hi - q_lo + 1;
+    if (nout <= 0) continue;
+    ConvArgs a{};
+    a.x = x; a.w = w_phases[r]; a.bias = bias; a.sa = snake_alpha_exp; a.sb = snake_inv_beta;
+    a.res = nullptr; a.y = y;
+    a.xbs = (long long)Cin * Tin; a.ybs = (long long)Cout * Tout; a.rbs = 0;
+    a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = nout;
+    // Kp-tap conv: tap j' reads input q - (Kp-1) + j' (weight W[ci][co][r + s*(Kp-1-j')]);
+    // q = n + q_lo
+    a.K = Kp; a.s = 1; a.d = 1; a.pl = Kp - 1 - q_lo;
+    a.yT = Tout; a.ostride = s; a.ooff = s * q_lo - p + r; a.epi = 0;
+    if (a.pl < 0) return BC_ERR_UNSUPPORTED;  // padding >= K: not a DecoderBlock shape
+    const int rc = conv_launch(a, B, cfg, S(stream));
+    if (rc != BC_OK) return rc;
+  }
+  return BC_OK;
+}
+
+int bc_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                 float* y, int B, int C, long long T, void* stream) {
+  if (!x || !y || !snake_alpha_exp || !snake_inv_beta || B < 0 || C <= 0 || T < 0) return BC_ERR_ARG;
+  return snake_launch(x, snake_alpha_exp, snake_inv_beta, y, B, C, T, S(stream));
+}
+
+int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                    const float* up_filter, const float* down_filter, float* y, int B, int C, int T,
+                    void* stream) {
+  if (!x || !y || !snake_alpha_exp || !snake_inv_beta || !up_filter || !down_filter || B < 0 ||
+      C <= 0 || T < 0)
+    return BC_ERR_ARG;
+  return aa_snake_launch(x, snake_alpha_exp, snake_inv_beta, up_filter, down_filter, y, B, C, T,
+                         S(stream));
+}
+
+long long bc_lstm_hh_packed_floats(int H) {
+  if (H <= 0 || H % 16) return -1;
+  return (long long)4 * H * H;
+}
+
+int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H) {
+  if (!w_hh_host || !packed_host || H <= 0 || H % 16) return BC_ERR_ARG;
+  lstm_pack_hh(w_hh_host, packed_host, H);
+  return BC_OK;
+}
+
+// workspace: xt [H][T*B] | gx [4H][T*B] | y0 [H][T*B] | y1 [H][T*B] | c [H][B]
+long long bc_lstm_workspace_floats(int B, int H, int T) {
+  if (B < 0 || H <= 0 || T < 0) return -1;
+  const long long tb = (long long)T * B;
+  return tb * H * 3 + tb * 4 * H + (long long)H * B;
+}
+
+int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
+                   const float* const* w_ih_packed, const float* const* bias,
+                   const float* const* w_hh_packed, float* workspace, void* stream) {
+  if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
+      H % 16 || T < 0 || num_layers <= 0)
+    return BC_ERR_ARG;
+  if (B == 0 || T == 0) return BC_OK;
+  hipStream_t st = S(stream);
+  const long long tb = (long long)T * B;
+  if (tb > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  float* xt = workspace;
+  float* gx = xt + tb * H;
+  float* ya = gx + tb * 4 * H;
+  float* yb = ya + tb * H;
+  float* cst = yb + tb * H;
+  int rc = btc_to_ctb_launch(x, xt, B, H, T, st);
+  if (rc) return rc;
+  const int cfg = conv_select_cfg(4 * H, H);
+  const float* lin = xt;
+  float* lout = ya;
+  for (int l = 0; l < num_layers; ++l) {
+    if (!w_ih_packed[l] || !w_hh_packed[l] || !bias[l]) return BC_ERR_ARG;
+    ConvArgs a{};
+    a.x = lin; a.w = w_ih_packed[l]; a.bias = bias[l]; a.sa = nullptr; a.sb = nullptr;
+    a.res = nullptr; a.y = gx;
+    a.xbs = 0; a.ybs = 0; a.rbs = 0;
+    a.Cin = H; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
+    a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
+    a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
+    rc = conv_launch(a, 1, cfg, st);
+    if (rc) return rc;
+    for (int t = 0; t < T; ++t) {
+      rc = lstm_step_launch(gx, w_hh_packed[l], lout, cst, H, B, T, t, st);
+      if (rc) return rc;
+    }
+    lin = lout;
+    lout = (lout == ya) ? yb : ya;
+  }
+  return ctb_to_btc_add_launch(lin, x, out, B, H, T, st);
+}
+
+int bc_vq_prepare_codebook(const float* codebook, float* codebook_norm, float* codebook_sq,
+                           int n_codes, int dim, void* stream) {
+  if (!codebook || !codebook_norm || !codebook_sq || n_codes <= 0) return BC_ERR_ARG;
+  if (dim != 8) return BC_ERR_UNSUPPORTED;
+  return vq_prepare_launch(codebook, codebook_norm, codebook_sq, n_codes, S(stream));
+}
+
+int bc_vq_fwd(const float* z, const float* w_in, const float* b_in, const float* codebook,
+              const float* codebook_norm, const float* codebook_sq, const float* w_out,
+              const float* b_out, long long* idx, float* z_e_out, float* post_out, int B, int D,
+              int T, int n_codes, int dim, void* stream) {
+  if (!z || !w_in || !b_in || !codebook || !codebook_norm || !codebook_sq || !idx || B < 0 ||
+      D <= 0 || T < 0 || n_codes <= 0)
+    return BC_ERR_ARG;
+  if (post_out && (!w_out || !b_out)) return BC_ERR_ARG;
+  if (dim != 8) return BC_ERR_UNSUPPORTED;
+  return vq_fwd_launch(z, w_in, b_in, codebook, codebook_norm, codebook_sq, w_out, b_out, idx,
+                       z_e_out, post_out, B, D, T, n_codes, S(stream));
+}
+
+int bc_vq_argmin(const float* z_e, const float* codebook_norm, const float* codebook_sq,
+                 long long* idx, long long N, int n_codes, int dim, void* stream) {
+  if (!z_e || !codebook_norm || !codebook_sq || !idx || N < 0 || n_codes <= 0) return BC_ERR_ARG;
+  if (dim != 8) return BC_ERR_UNSUPPORTED;
+  return vq_argmin_launch(z_e, codebook_norm, codebook_sq, idx, N, n_codes, S(stream));
+}
+
+int bc_vq2emb(const long long* idx, long long idx_stride, const float* codebook,
+              const float* w_out, const float* b_out, float* emb, long long N, int D, int n_codes,
+              int dim, int accumulate, void* stream) {
+  if (!idx || idx_stride <= 0 || !codebook || !emb || N < 0 || D <= 0 || n_codes <= 0)
+    return BC_ERR_ARG;
+  if ((w_out == nullptr) != (b_out == nullptr)) return BC_ERR_ARG;
+  if (!w_out && D != dim) return BC_ERR_ARG;
+  if (dim != 8) return BC_ERR_UNSUPPORTED;
+  return vq2emb_launch(idx, idx_stride, codebook, w_out, b_out, emb, N, D, accumulate, S(stream));
+}
+
+int bc_rvq_update(float* residual, float* out, const float* q, long long n, int first,
+                  void* stream) {
+  if (!residual || !out || !q || n < 0) return BC_ERR_ARG;
+  return rvq_update_launch(residual, out, q, n, first, S(stream));
+}
+
+int bc_btc_to_ctb(const float* x, float* y, int B, int C, int T, void* stream) {
+  if (!x || !y || B < 0 || C < 0 || T < 0) return BC_ERR_ARG;
+  return btc_to_ctb_launch(x, y, B, C, T, S(stream));
+}
+
+int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int C, int T,
+                      void* stream) {
+  if (!y || !skip || !out || B < 0 || C < 0 || T < 0) return BC_ERR_ARG;
+  return ctb_to_btc_add_launch(y, skip, out, B, C, T, S(stream));
+}
+
+int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream) {
+  if (!x || B < 0 || T < 0 || clip0 < 0) return BC_ERR_ARG;
+  return synth_clips_launch(x, B, T, clip0, S(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,52 @@
+// Host-side launchers shared between the kernel translation units and the C ABI (abi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace bc {
+struct ConvArgs {
+  const float* x;
+  const float* w;
+  const float* bias;
+  const float* sa;
+  const float* sb;
+  const float* res;
+  float* y;
+  long long xbs, ybs, rbs;
+  int Cin, Tin, Cout, Nout;
+  int K, s, d, pl;
+  int yT, ostride, ooff;
+  int epi;
+  int nchunks, win;
+  int ntm, ntn, nwg;
+};
+int conv_select_cfg(int Cout, int Cin);
+long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id);
+void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id);
+int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
+
+int snake_launch(const float* x, const float* sa, const float* sb, float* y, int B, int C,
+                 long long T, hipStream_t st);
+int aa_snake_launch(const float* x, const float* sa, const float* sb, const float* fu,
+                    const float* fd, float* y, int B, int C, int T, hipStream_t st);
+int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t st);
+int ctb_to_btc_add_launch(const float* y, const float* skip, float* out, int B, int C, int T,
+                          hipStream_t st);
+int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st);
+
+void lstm_pack_hh(const float* w, float* out, int H);
+int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
+                     int T, int t, hipStream_t st);
+
+int vq_prepare_launch(const float* cb, float* cbn, float* csq, int n, hipStream_t st);
+int vq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* cb,
+                  const float* cbn, const float* csq, const float* w_out, const float* b_out,
+                  long long* idx, float* ze_out, float* post, int B, int D, int T, int ncodes,
+                  hipStream_t st);
+int vq_argmin_launch(const float* ze, const float* cbn, const float* csq, long long* idx,
+                     long long N, int ncodes, hipStream_t st);
+int vq2emb_launch(const long long* idx, long long idx_stride, const float* cb, const float* w_out,
+                  const float* b_out, float* emb, long long N, int D, int accumulate,
+                  hipStream_t st);
+int rvq_update_launch(float* residual, float* out, const float* q, long long n, int first,
+                      hipStream_t st);
+}  // namespace bc

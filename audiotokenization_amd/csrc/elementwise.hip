@@ -1,0 +1,207 @@
+// HBM-bound elementwise / resampling kernels.
+//
+//  snake_kernel     : SnakeBeta alone (vq/activations.py:107-118) for a standalone Activation1d /
+//                     SnakeBeta module call.  Inside the encoder/decoder stacks the Snake is fused
+//                     into the following conv's input staging instead (conv1d.hip).
+//  aa_snake_kernel  : Activation1d with antialias=True (vq/alias_free_torch/act.py:25-32):
+//                     UpSample1d (resample.py:25-33: replicate pad 5, depthwise 12-tap transposed
+//                     conv stride 2, x2 gain, crop [15:-15]) -> SnakeBeta -> DownSample1d
+//                     (filter.py:86-95: replicate pad (5,6), depthwise 12-tap conv stride 2), fused so
+//                     the 2T intermediate never leaves LDS.
+//  transpose kernels: [B][C][T] <-> [C][T][B] layouts around the ResLSTM (vq/module.py:160-166).
+//  synth_clips      : counter-hash white noise generated in HBM.
+#include "bc_common.h"
+#include "bc_internal.h"
+
+namespace bc {
+
+__global__ void snake_kernel(const float* __restrict__ x, const float* __restrict__ sa,
+                             const float* __restrict__ sb, float* __restrict__ y, int C, long long T,
+                             long long total) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)((i / T) % C);
+    y[i] = snake(x[i], sa[c], sb[c]);
+  }
+}
+
+// One workgroup = one (b, c) row segment of AA_TILE outputs.
+constexpr int AA_TILE = 256;
+constexpr int AA_TAPS = 12;
+
+__global__ void __launch_bounds__(256) aa_snake_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ sa,
+                                                       const float* __restrict__ sb,
+                                                       const float* __restrict__ fup,
+                                                       const float* __restrict__ fdown,
+                                                       float* __restrict__ y, int C, int T,
+                                                       int ntiles) {
+  __shared__ float xl[AA_TILE / 2 + AA_TILE + 32];
+  __shared__ float sl[2 * AA_TILE + 16];
+  __shared__ float fu[AA_TAPS], fd[AA_TAPS];
+  const int tile = blockIdx.x % ntiles;
+  const long long row = blockIdx.x / ntiles;  // b*C + c
+  const int c = (int)(row % C);
+  const float* xr = x + row * T;
+  float* yr = y + row * T;
+  const int t0 = tile * AA_TILE;
+  if (threadIdx.x < AA_TAPS) {
+    fu[threadIdx.x] = fup[threadIdx.x];
+    fd[threadIdx.x] = fdown[threadIdx.x];
+  }
+  // Down stage needs snake values at up-sample index v in [2*t0-5, 2*t0+2*AA_TILE+5].
+  // Up-sample index v (after the [15:-15] crop) = u - 15 where u indexes the transposed-conv
+  // output; u = 2*i + k with i indexing the replicate-padded input x_p[i] = x[clamp(i-5)].
+  const int vbase = 2 * t0 - 5;
+  const int nv = 2 * AA_TILE + 11;
+  // input indices needed: i = (v + 15 - k)/2 for k in [0,12): i in [(vbase+4)/2, (vmax+15)/2]
+  const int ibase = (vbase + 15 - 11) >> 1;  // floor, vbase+4 may be negative -> arithmetic shift
+  const int ni = (nv + 12) / 2 + 2;
+  for (int e = threadIdx.x; e < ni; e += 256) {
+    int xi = ibase + e - 5;
+    xi = xi < 0 ? 0 : (xi >= T ? T - 1 : xi);
+    xl[e] = xr[xi];
+  }
+  __syncthreads();
+  const float a = sa[c], ib = sb[c];
+  for (int e = threadIdx.x; e < nv; e += 256) {
+    int v = vbase + e;
+    v = v < 0 ? 0 : (v >= 2 * T ? 2 * T - 1 : v);  // replicate pad of the snake output (down stage)
+    const int u = v + 15;
+    float acc = 0.f;
+    // conv_transpose1d: out[u] = sum_{k: (u-k) even} x_p[(u-k)/2] * f[k]
+#pragma unroll
+    for (int k = (u & 1); k < AA_TAPS; k += 2) {
+      const int i = (u - k) >> 1;
+      acc = acc + xl[i - ibase] * fu[k];
+    }
+    const float up = 2.0f * acc;
+    sl[e] = snake(up, a, ib);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < AA_TILE; e += 256) {
+    const int t = t0 + e;
+    if (t >= T) break;
+    // out[t] = sum_k z_p[2t+k] f[k], z_p[j] = s[clamp(j-5)]  -> s index v = 2t+k-5
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < AA_TAPS; ++k) acc = acc + sl[2 * e + k] * fd[k];
+    yr[t] = acc;
+  }
+}
+
+// x[B][C][T] -> y[C][T][B]   (tiles of 32 t x B<=64 per channel)
+__global__ void __launch_bounds__(256) btc_to_ctb_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ y, int B, int C,
+                                                         int T) {
+  __shared__ float tl[64][33];
+  const int tt = blockIdx.x;  // t-tile of 32
+  const int c = blockIdx.y;
+  const int bt = blockIdx.z;  // b-tile of 64
+  const int t0 = tt * 32, b0 = bt * 64;
+  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    const int bl = e / 32, tl_ = e % 32;
+    const int b = b0 + bl, t = t0 + tl_;
+    tl[bl][tl_] = (b < B && t < T) ? x[((long long)b * C + c) * T + t] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    const int tl_ = e / 64, bl = e % 64;
+    const int b = b0 + bl, t = t0 + tl_;
+    if (b < B && t < T) y[((long long)c * T + t) * B + b] = tl[bl][tl_];
+  }
+}
+
+// out[B][C][T] = y[C][T][B] + skip[B][C][T]   (ResLSTM skip, vq/module.py:163-166)
+__global__ void __launch_bounds__(256) ctb_to_btc_add_kernel(const float* __restrict__ yin,
+                                                             const float* __restrict__ skip,
+                                                             float* __restrict__ out, int B, int C,
+                                                             int T) {
+  __shared__ float tl[64][33];
+  const int tt = blockIdx.x, c = blockIdx.y, bt = blockIdx.z;
+  const int t0 = tt * 32, b0 = bt * 64;
+  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    const int tl_ = e / 64, bl = e % 64;
+    const int b = b0 + bl, t = t0 + tl_;
+    tl[bl][tl_] = (b < B && t < T) ? yin[((long long)c * T + t) * B + b] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    const int bl = e / 32, tl_ = e % 32;
+    const int b = b0 + bl, t = t0 + tl_;
+    if (b < B && t < T) {
+      const long long i = ((long long)b * C + c) * T + t;
+      out[i] = tl[bl][tl_] + skip[i];
+    }
+  }
+}
+
+// Clip i, sample n: u = (splitmix64(0xB16C0DEC ^ (i<<32) ^ n) >> 40) * 2^-24, x = u - 0.5.
+__global__ void synth_clips_kernel(float* __restrict__ x, int B, long long T, long long clip0) {
+  const long long total = (long long)B * T;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const unsigned long long i = (unsigned long long)(clip0 + e / T);
+    const unsigned long long n = (unsigned long long)(e % T);
+    const unsigned long long h = splitmix64(0xB16C0DECull ^ (i << 32) ^ n);
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    x[e] = u - 0.5f;
+  }
+}
+
+static inline int grid_for(long long n, int block) {
+  long long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+int snake_launch(const float* x, const float* sa, const float* sb, float* y, int B, int C,
+                 long long T, hipStream_t st) {
+  const long long total = (long long)B * C * T;
+  if (total == 0) return BC_OK;
+  hipLaunchKernelGGL(snake_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, sa, sb, y, C, T,
+                     total);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int aa_snake_launch(const float* x, const float* sa, const float* sb, const float* fu,
+                    const float* fd, float* y, int B, int C, int T, hipStream_t st) {
+  if ((long long)B * C * T == 0) return BC_OK;
+  const int ntiles = (T + AA_TILE - 1) / AA_TILE;
+  const long long nwg = (long long)B * C * ntiles;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  hipLaunchKernelGGL(aa_snake_kernel, dim3((unsigned)nwg), dim3(256), 0, st, x, sa, sb, fu, fd, y, C,
+                     T, ntiles);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t st) {
+  if ((long long)B * C * T == 0) return BC_OK;
+  dim3 grid((T + 31) / 32, C, (B + 63) / 64);
+  hipLaunchKernelGGL(btc_to_ctb_kernel, grid, dim3(256), 0, st, x, y, B, C, T);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int ctb_to_btc_add_launch(const float* y, const float* skip, float* out, int B, int C, int T,
+                          hipStream_t st) {
+  if ((long long)B * C * T == 0) return BC_OK;
+  dim3 grid((T + 31) / 32, C, (B + 63) / 64);
+  hipLaunchKernelGGL(ctb_to_btc_add_kernel, grid, dim3(256), 0, st, y, skip, out, B, C, T);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st) {
+  const long long total = (long long)B * T;
+  if (total == 0) return BC_OK;
+  hipLaunchKernelGGL(synth_clips_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, B, T,
+                     clip0);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+}  // namespace bc

@@ -1,0 +1,264 @@
+// Factorized VQ (vq/factorized_vector_quantize.py:29-108) for codebook_dim = 8.
+//
+//  vq_prepare_codebook_kernel : F.normalize(codebook) and codebook.pow(2).sum(1) (:99, :105).
+//  vq_fwd_kernel              : per frame: in_proj (WN Linear D->8, :56) -> F.normalize (:98) ->
+//                               dist = sum(e^2) - 2 e.c + sum(c^2) (:102-106) -> first argmin
+//                               (== (-dist).max(1)[1], :107) -> z_q = codebook[idx] (:108) ->
+//                               z_e + (z_q - z_e) (:68-70) -> out_proj (WN Linear 8->D, :72-74).
+//  vq_argmin_kernel           : the search alone on given projected latents z_e.
+//  vq2emb_kernel              : indices -> out_proj(codebook[idx]) (:78-91, residual_vq.py:42-48).
+//
+// Bit-exactness contract (tests/test_vq_*): given the same z_e, the indices equal the reference's.
+// The fp32 operation order below restates what torch's CPU kernels do for these shapes, verified
+// element-for-element in this container (oracle/vq_oracle.c header):
+//   ||x||   = sqrt(((x0*x0 + x1*x1) + x2*x2) + ...)   sequential, separately rounded mul/add
+//   e       = x / max(||x||, 1e-12)                    correctly rounded division
+//   sum e^2 = sequential mul/add as above
+//   e.c     = fma chain over k = 0..7 starting from 0 (MKL sgemm, K=8, >= 2 rows)
+//   dist    = (sum_e2 - 2*dot) + sum_c2
+// The library is built with -ffp-contract=off, so none of these are contracted.
+#include "bc_common.h"
+#include "bc_internal.h"
+
+namespace bc {
+
+constexpr int VQ_DIM = 8;
+
+__device__ __forceinline__ void normalize8(float (&v)[VQ_DIM]) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VQ_DIM; ++k) s = s + v[k] * v[k];
+  float n = sqrtf(s);
+  const float eps = 1e-12f;
+  n = n < eps ? eps : n;  // clamp_min(eps); a NaN norm propagates as in torch's clamp_min
+#pragma unroll
+  for (int k = 0; k < VQ_DIM; ++k) v[k] = v[k] / n;
+}
+
+__device__ __forceinline__ float sumsq8(const float (&v)[VQ_DIM]) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VQ_DIM; ++k) s = s + v[k] * v[k];
+  return s;
+}
+
+__global__ void vq_prepare_codebook_kernel(const float* __restrict__ cb, float* __restrict__ cbn,
+                                           float* __restrict__ csq, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v[VQ_DIM];
+#pragma unroll
+  for (int k = 0; k < VQ_DIM; ++k) v[k] = cb[(long long)i * VQ_DIM + k];
+  normalize8(v);
+#pragma unroll
+  for (int k = 0; k < VQ_DIM; ++k) cbn[(long long)i * VQ_DIM + k] = v[k];
+  csq[i] = sumsq8(v);
+}
+
+constexpr int VQ_CHUNK = 1024;  // codes staged per LDS pass (1024 * 9 floats = 36 KB)
+
+// Search the whole codebook for one normalized row e (per lane); codes are staged into LDS in
+// chunks and read by every lane at the same address (LDS broadcast).
+__device__ __forceinline__ int vq_search(const float (&e)[VQ_DIM], float se,
+                                         const float* __restrict__ cbn,
+                                         const float* __restrict__ csq, int ncodes, float* lds_cb,
+                                         float* lds_sq) {
+  float best = __builtin_huge_valf();
+  int bidx = 0;
+  bool first = true;
+  for (int c0 = 0; c0 < ncodes; c0 += VQ_CHUNK) {
+    const int cn = min(VQ_CHUNK, ncodes - c0);
+    __syncthreads();
+    for (int q = threadIdx.x; q < cn * VQ_DIM; q += blockDim.x) lds_cb[q] = cbn[(long long)c0 * VQ_DIM + q];
+    for (int q = threadIdx.x; q < cn; q += blockDim.x) lds_sq[q] = csq[c0 + q];
+    __syncthreads();
+    for (int k = 0; k < cn; ++k) {
+      const float* c = lds_cb + k * VQ_DIM;
+      float dot = 0.f;
+#pragma unroll
+      for (int q = 0; q < VQ_DIM; ++q) dot = fmaf(e[q], c[q], dot);
+      const float dist = (se - 2.0f * dot) + lds_sq[k];
+      // first index of the maximum of -dist: strict '<' keeps the earliest code on ties.  A NaN
+      // distance never wins a comparison; torch's max() would propagate it, which cannot happen
+      // for finite latents.
+      if (first || dist < best) {
+        best = dist;
+        bidx = c0 + k;
+        first = false;
+      }
+    }
+  }
+  return bidx;
+}
+
+// One thread per frame n = b*T + t.  z: [B][D][T]; outputs idx[B*T] (int64), optional
+// z_e[B][8][T], optional post[B][D][T].
+__global__ void __launch_bounds__(256) vq_fwd_kernel(
+    const float* __restrict__ z, const float* __restrict__ w_in, const float* __restrict__ b_in,
+    const float* __restrict__ cb, const float* __restrict__ cbn, const float* __restrict__ csq,
+    const float* __restrict__ w_out, const float* __restrict__ b_out, long long* __restrict__ idx,
+    float* __restrict__ ze_out, float* __restrict__ post, int B, int D, int T, int ncodes) {
+  __shared__ float lds_cb[VQ_CHUNK * VQ_DIM];
+  __shared__ float lds_sq[VQ_CHUNK];
+  const long long NF = (long long)B * T;
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = n < NF;
+  const long long nn = live ? n : NF - 1;
+  const int b = (int)(nn / T), t = (int)(nn % T);
+  const float* zb = z + (long long)b * D * T + t;
+
+  // in_proj: z_e[j] = sum_d W[j][d] z[d] + bias[j]
+  float ze[VQ_DIM];
+#pragma unroll
+  for (int q = 0; q < VQ_DIM; ++q) ze[q] = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float zv = zb[(long long)d * T];
+#pragma unroll
+    for (int q = 0; q < VQ_DIM; ++q) ze[q] = fmaf(w_in[q * D + d], zv, ze[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < VQ_DIM; ++q) ze[q] = ze[q] + b_in[q];
+  if (ze_out && live)
+#pragma unroll
+    for (int q = 0; q < VQ_DIM; ++q) ze_out[((long long)b * VQ_DIM + q) * T + t] = ze[q];
+
+  float e[VQ_DIM];
+#pragma unroll
+  for (int q = 0; q < VQ_DIM; ++q) e[q] = ze[q];
+  normalize8(e);
+  const float se = sumsq8(e);
+  const int k = vq_search(e, se, cbn, csq, ncodes, lds_cb, lds_sq);
+  if (!live) return;
+  idx[n] = k;
+  if (post) {
+    float st[VQ_DIM];
+#pragma unroll
+    for (int q = 0; q < VQ_DIM; ++q) {
+      const float zq = cb[(long long)k * VQ_DIM + q];
+      st[q] = ze[q] + (zq - ze[q]);  // straight-through, forward value
+    }
+    float* pb = post + (long long)b * D * T + t;
+    for (int d = 0; d < D; ++d) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < VQ_DIM; ++q) acc = fmaf(w_out[d * VQ_DIM + q], st[q], acc);
+      pb[(long long)d * T] = acc + b_out[d];
+    }
+  }
+}
+
+// z_e rows [N][8] -> idx[N]
+__global__ void __launch_bounds__(256) vq_argmin_kernel(const float* __restrict__ ze,
+                                                        const float* __restrict__ cbn,
+                                                        const float* __restrict__ csq,
+                                                        long long* __restrict__ idx, long long N,
+                                                        int ncodes) {
+  __shared__ float lds_cb[VQ_CHUNK * VQ_DIM];
+  __shared__ float lds_sq[VQ_CHUNK];
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nn = n < N ? n : N - 1;
+  float e[VQ_DIM];
+#pragma unroll
+  for (int q = 0; q < VQ_DIM; ++q) e[q] = ze[nn * VQ_DIM + q];
+  normalize8(e);
+  const float se = sumsq8(e);
+  const int k = vq_search(e, se, cbn, csq, ncodes, lds_cb, lds_sq);
+  if (n < N) idx[n] = k;
+}
+
+// emb[n][d] = b_out[d] + sum_q W_out[d][q] * cb[idx[n]][q]     (output (N, D), as vq2emb returns)
+__global__ void vq2emb_kernel(const long long* __restrict__ idx, long long idx_stride,
+                              const float* __restrict__ cb, const float* __restrict__ w_out,
+                              const float* __restrict__ b_out, float* __restrict__ emb, long long N,
+                              int D, int accumulate) {
+  const long long total = N * D;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const long long n = e / D;
+    const int d = (int)(e % D);
+    const long long k = idx[n * idx_stride];
+    float v;
+    if (w_out) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < VQ_DIM; ++q) acc = fmaf(w_out[d * VQ_DIM + q], cb[k * VQ_DIM + q], acc);
+      v = acc + b_out[d];
+    } else {
+      v = cb[k * VQ_DIM + d];  // proj=False: embed_code only
+    }
+    emb[e] = accumulate ? emb[e] + v : v;
+  }
+}
+
+// ResidualVQ bookkeeping (residual_vq.py:31-33): residual -= q; out += q
+__global__ void rvq_update_kernel(float* __restrict__ residual, float* __restrict__ out,
+                                  const float* __restrict__ q, long long n, int first) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float qi = q[i];
+    residual[i] = residual[i] - qi;
+    out[i] = first ? 0.f + qi : out[i] + qi;
+  }
+}
+
+static inline int grid_for(long long n, int block) {
+  long long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+int vq_prepare_launch(const float* cb, float* cbn, float* csq, int n, hipStream_t st) {
+  if (n <= 0) return BC_ERR_ARG;
+  hipLaunchKernelGGL(vq_prepare_codebook_kernel, dim3((n + 255) / 256), dim3(256), 0, st, cb, cbn,
+                     csq, n);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int vq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* cb,
+                  const float* cbn, const float* csq, const float* w_out, const float* b_out,
+                  long long* idx, float* ze_out, float* post, int B, int D, int T, int ncodes,
+                  hipStream_t st) {
+  const long long NF = (long long)B * T;
+  if (NF == 0) return BC_OK;
+  const long long nwg = (NF + 255) / 256;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  hipLaunchKernelGGL(vq_fwd_kernel, dim3((unsigned)nwg), dim3(256), 0, st, z, w_in, b_in, cb, cbn,
+                     csq, w_out, b_out, idx, ze_out, post, B, D, T, ncodes);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int vq_argmin_launch(const float* ze, const float* cbn, const float* csq, long long* idx,
+                     long long N, int ncodes, hipStream_t st) {
+  if (N == 0) return BC_OK;
+  const long long nwg = (N + 255) / 256;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  hipLaunchKernelGGL(vq_argmin_kernel, dim3((unsigned)nwg), dim3(256), 0, st, ze, cbn, csq, idx, N,
+                     ncodes);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int vq2emb_launch(const long long* idx, long long idx_stride, const float* cb, const float* w_out,
+                  const float* b_out, float* emb, long long N, int D, int accumulate,
+                  hipStream_t st) {
+  const long long total = N * D;
+  if (total == 0) return BC_OK;
+  hipLaunchKernelGGL(vq2emb_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, idx, idx_stride, cb,
+                     w_out, b_out, emb, N, D, accumulate);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int rvq_update_launch(float* residual, float* out, const float* q, long long n, int first,
+                      hipStream_t st) {
+  if (n == 0) return BC_OK;
+  hipLaunchKernelGGL(rvq_update_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, residual, out, q,
+                     n, first);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+}  // namespace bc

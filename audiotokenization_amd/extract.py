@@ -1,0 +1,173 @@
+"""extract_indices-equivalent driver (extract_indices.py:281-589) on the HIP path.
+
+  * index post-processing and on-disk format (extract_indices.py:512-561): codes (Nq, 1, F) ->
+    squeeze(1) -> permute to (F, Nq) -> int16 -> np.save(<out>/<subset>/<spk>/<chapter>/<fileid>.npy)
+  * clip-sharded data-parallel extraction: global clip ids are block-partitioned
+    over ranks, each rank encodes its own batches, and the batch's int64 index tensor is
+    all-gathered over the process group (RCCL over xGMI on MI355X, gloo on CPU test runs).
+  * per-item error accounting (extract_indices.py:565-574): failures are counted, not fatal.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def indices_to_numpy(indices: torch.Tensor) -> np.ndarray:
+    """extract_indices.py:520-532 for one clip: (Nq, 1, F) -> (F, Nq) int16 (or (F,) from (1, F))."""
+    indices = indices.squeeze(1)
+    if indices.ndim == 2:
+        indices = indices.permute(1, 0)
+    elif indices.ndim != 1:
+        raise ValueError(f"Unexpected indices dimension: {indices.ndim}")
+    return indices.cpu().numpy().astype(np.int16)
+
+
+def batch_indices_to_numpy(codes: torch.Tensor) -> np.ndarray:
+    """(Nq, B, F) -> (B, F, Nq) int16; row b equals indices_to_numpy(codes[:, b:b+1])."""
+    if codes.ndim != 3:
+        raise ValueError("codes must be (Nq, B, F)")
+    return codes.permute(1, 2, 0).cpu().numpy().astype(np.int16)
+
+
+def parse_fileid(fileid: str) -> Tuple[str, str]:
+    """extract_indices.py:536-548: speaker / chapter from a LibriTTS / LibriSpeech file id."""
+    if "_" in fileid:
+        parts = fileid.split("_")
+        return parts[0], parts[1]
+    if "-" in fileid:
+        parts = fileid.split("-")
+        return parts[0], parts[1]
+    return "unknown", "unknown"
+
+
+def output_path(output_dir: str, subset: str, fileid: str) -> str:
+    """extract_indices.py:551-558."""
+    spk, ch = parse_fileid(fileid)
+    return os.path.join(output_dir, subset, spk, ch, f"{fileid}.npy")
+
+
+def save_indices(output_dir: str, subset: str, fileid: str, indices_np: np.ndarray) -> str:
+    path = output_path(output_dir, subset, fileid)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    np.save(path, indices_np)
+    return path
+
+
+class BigCodecModel(torch.nn.Module):
+    """extract_indices.py:281-371 / inference_full.py:535-561 wrapper around a CodecLightningModule."""
+
+    def __init__(self, lm, reconstruct: bool = False):
+        super().__init__()
+        self.lm = lm
+        self.reconstruct = reconstruct
+        self.codebook_size = lm.cfg.model.codec_decoder.codebook_size
+
+    @torch.no_grad()
+    def forward(self, x):
+        vq_emb = self.lm.model["CodecEnc"](x)
+        vq_post_emb, vq_code, _ = self.lm.model["generator"](vq_emb, vq=True)
+        if not self.reconstruct:
+            return {"indices": vq_code}
+        recon = self.lm.model["generator"](vq_post_emb, vq=False)
+        return {"x_rec": recon, "indices": vq_code, "loss": {}}
+
+
+def pad_like_inference_full(x: torch.Tensor, hop: int = 200) -> torch.Tensor:
+    """inference_full.py:712: F.pad(x, (0, hop - T % hop)) — always pads (a full hop when T is
+    already a multiple).  Allocation + copy only."""
+    B, C, T = x.shape
+    pad = hop - (T % hop)
+    out = torch.zeros((B, C, T + pad), device=x.device, dtype=x.dtype)
+    out[..., :T] = x
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# clip-sharded data-parallel extraction
+# ------------------------------------------------------------------------------------------------
+def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
+    """Block partition of [0, n_items): rank r gets [r*n/W, (r+1)*n/W)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    lo = (n_items * rank) // world
+    hi = (n_items * (rank + 1)) // world
+    return lo, hi
+
+
+def batches(lo: int, hi: int, batch: int) -> List[Tuple[int, int]]:
+    return [(s, min(s + batch, hi)) for s in range(lo, hi, batch)]
+
+
+def synth_batch(n_clips: int, n_samples: int, clip0: int, device) -> torch.Tensor:
+    """White-noise clips (B, 1, T) generated in HBM by bc_synth_clips (same values as synth.synth_clips)."""
+    x = torch.empty((n_clips, 1, n_samples), device=device, dtype=torch.float32)
+    L.call("bc_synth_clips", x.data_ptr(), n_clips, n_samples, clip0, L.stream_of(x))
+    return x
+
+
+def all_gather_codes(codes: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather one batch's (Nq, B, F) int64 codes over the process group -> (W, Nq, B, F).
+    Ranks must pass equal shapes (pad the last batch)."""
+    import torch.distributed as dist
+
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return codes.unsqueeze(0)
+    world = dist.get_world_size(group)
+    codes = codes.contiguous()
+    out = torch.empty((world * codes.shape[0],) + tuple(codes.shape[1:]), dtype=codes.dtype, device=codes.device)
+    dist.all_gather_into_tensor(out, codes, group=group)
+    return out.view((world,) + tuple(codes.shape))
+
+
+@dataclass
+class ExtractStats:
+    clips: int = 0
+    errors: int = 0
+    frames: int = 0
+    error_items: List[int] = field(default_factory=list)
+
+
+def extract_sharded(model: BigCodecModel, n_clips: int, n_samples: int, batch: int, rank: int = 0,
+                    world: int = 1, device=None, gather: bool = True, sink=None, group=None) -> ExtractStats:
+    """Encode clips [0, n_clips) clip-sharded over `world` ranks (synthetic corpus, config 4).
+
+    Every rank runs the same number of batches (the last one padded with clip ids that are
+    discarded) so the per-batch all-gather lines up.  `sink(global_clip_ids, codes_np)` receives the
+    gathered (n, F, Nq) int16 arrays on rank 0 (e.g. an .npy writer)."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    lo, hi = shard_range(n_clips, rank, world)
+    per_rank = max(shard_range(n_clips, r, world)[1] - shard_range(n_clips, r, world)[0] for r in range(world))
+    n_batches = (per_rank + batch - 1) // batch
+    stats = ExtractStats()
+    for bi in range(n_batches):
+        s = lo + bi * batch
+        e = min(s + batch, hi)
+        real = max(0, e - s)
+        x = synth_batch(batch, n_samples, s, device)
+        try:
+            codes = model(x)["indices"]
+        except Exception:  # per-batch accounting, mirrors extract_indices.py:565-574
+            stats.errors += real
+            stats.error_items.extend(range(s, e))
+            codes = None
+        if codes is None:
+            continue
+        stats.clips += real
+        stats.frames += real * codes.shape[-1]
+        gathered = all_gather_codes(codes, group) if gather else codes.unsqueeze(0)
+        if sink is not None and rank == 0:
+            arr = gathered.permute(0, 2, 3, 1).cpu().numpy().astype(np.int16)  # (W, B, F, Nq)
+            for r in range(gathered.shape[0]):
+                rlo, rhi = shard_range(n_clips, r, world) if gather else (lo, hi)
+                rs = rlo + bi * batch
+                for j in range(batch):
+                    if rs + j < rhi:
+                        sink(rs + j, arr[r, j])
+    return stats

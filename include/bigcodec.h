@@ -1,0 +1,132 @@
+/*
+ * bigcodec.h — C ABI of libbigcodec_hip.so, the MI355X (gfx950) BigCodec tokenization hot path.
+ *
+ * The reference (hoyso48/AudioTokenization, BigCodec_SSL/) is pure PyTorch and has no FFI: its
+ * boundary is the nn.Module call surface of vq/codec_encoder.py, vq/codec_decoder.py and the
+ * modules they compose.  Each entry point below replaces one aten call chain behind one of those
+ * modules (cited per function).  The Python package audiotokenization_amd binds them with ctypes
+ * (INTEGRATION.md shows the binding) and mirrors the reference modules on top.
+ *
+ * Conventions
+ *   - every pointer argument named x/y/z/... is DEVICE memory (fp32 unless stated) and contiguous in
+ *     the stated layout; pointers named *_host are host memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream); all launches are
+ *     stream-ordered and asynchronous; no function allocates, frees or synchronises;
+ *   - return value: 0 = ok, 1 = bad argument, 2 = HIP launch error, 3 = unsupported shape.
+ *   - activations are [B][C][T] (batch, channel, time) as in the reference's Conv1d tensors.
+ */
+#ifndef BIGCODEC_H
+#define BIGCODEC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BC_ABI_VERSION 1
+
+int bc_abi_version(void);
+
+/* ---- Conv1d (weight-normed, optional fused SnakeBeta prologue / residual / tanh epilogue) ------
+ * Replaces: F.pad + conv1d of CausalConv1d.forward (vq/module.py:45-48) and weight_norm(nn.Conv1d)
+ * (vq/module.py:59-65), preceded by Activation1d(SnakeBeta) (vq/alias_free_torch/act.py:25-32,
+ * vq/activations.py:107-118) when snake_alpha_exp != NULL, followed by ResidualUnit's `x + ...`
+ * (vq/module.py:88-89) when residual != NULL and by nn.Tanh (vq/codec_decoder.py:80) when
+ * epilogue == 1.
+ *   y[b,co,n] = bias[co] + sum_{ci,k} W[co,ci,k] * snake(x[b,ci, n*stride + k*dilation - pad_left])
+ * with out-of-range input samples read as 0 (zero padding).  Non-causal: pad_left = padding;
+ * causal: pad_left = (K - stride) * dilation (vq/module.py:43).
+ * W is the FOLDED weight g*v/||v|| packed by bc_conv1d_pack for tile config `cfg`
+ * (cfg = bc_conv1d_select_cfg(Cout, Cin)).
+ * snake_alpha_exp[c] = exp(alpha[c]); snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9). */
+int bc_conv1d_select_cfg(int Cout, int Cin);
+long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg);
+int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg);
+int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias,
+                  const float* snake_alpha_exp, const float* snake_inv_beta,
+                  const float* residual, float* y,
+                  int B, int Cin, int Tin, int Cout, int Tout,
+                  int K, int stride, int dilation, int pad_left, int epilogue, int cfg,
+                  void* stream);
+
+/* ---- ConvTranspose1d (weight-normed, optional fused SnakeBeta prologue) ------------------------
+ * Replaces: weight_norm(nn.ConvTranspose1d) (vq/module.py:67-72) and CausalConvTranspose1d
+ * (vq/module.py:50-57, crop of the last `stride` samples) inside DecoderBlock (vq/module.py:
+ * 115-141) (DecoderBlock uses K = 2*stride).  Run as `stride` polyphase convolutions with
+ * Kp = bc_convT1d_phase_taps(K, stride) = ceil(K/stride) taps: phase r has
+ * W_r[co][ci][j'] = W[ci][co][r + stride*(Kp-1-j')] (0 where that tap index >= K), packed with
+ * bc_conv1d_pack(..., K=Kp, cfg).  w_phases is a HOST array of `stride` device pointers.
+ * Output length Tout = (Tin-1)*stride - 2*padding + K + output_padding (the caller passes Tout,
+ * which carries output_padding); DecoderBlock non-causal: padding = stride/2 + stride%2,
+ * output_padding = stride%2.  Causal (crop of the last `stride` samples): padding = 0,
+ * Tout = (Tin-1)*stride + K - stride. */
+int bc_convT1d_phase_taps(int K, int stride);
+int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bias,
+                   const float* snake_alpha_exp, const float* snake_inv_beta, float* y,
+                   int B, int Cin, int Tin, int Cout, int Tout, int K, int stride, int padding,
+                   int cfg, void* stream);
+
+/* ---- SnakeBeta / anti-aliased Activation1d -------------------------------------------------------
+ * bc_snake_fwd replaces SnakeBeta.forward (vq/activations.py:107-118).
+ * bc_aa_snake_fwd replaces Activation1d.forward with antialias=True (vq/alias_free_torch/act.py:
+ * 25-32): UpSample1d (resample.py:25-33) -> SnakeBeta -> DownSample1d (resample.py:47-49,
+ * filter.py:86-95).  up_filter / down_filter: the 12-tap buffers `upsample.filter` and
+ * `downsample.lowpass.filter` (device, 12 floats each). */
+int bc_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                 float* y, int B, int C, long long T, void* stream);
+int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                    const float* up_filter, const float* down_filter, float* y,
+                    int B, int C, int T, void* stream);
+
+/* ---- ResLSTM ----------------------------------------------------------------------------------------
+ * Replaces ResLSTM.forward (vq/module.py:156-167): rearrange b f t -> b t f, nn.LSTM(H, H,
+ * num_layers, batch_first=True) (unidirectional), + skip, rearrange back.  x, out: [B][H][T].
+ * Per layer l: w_ih_packed[l] = bc_conv1d_pack(weight_ih_l{l} as [4H][H][1], cfg =
+ * bc_conv1d_select_cfg(4H, H)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
+ * w_hh_packed[l] = bc_lstm_pack_hh(weight_hh_l{l}).  The three pointer arrays are HOST arrays of
+ * device pointers.  workspace: bc_lstm_workspace_floats(B, H, T) device floats.  H % 16 == 0. */
+long long bc_lstm_hh_packed_floats(int H);
+int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H);
+long long bc_lstm_workspace_floats(int B, int H, int T);
+int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
+                   const float* const* w_ih_packed, const float* const* bias,
+                   const float* const* w_hh_packed, float* workspace, void* stream);
+
+/* ---- Factorized VQ (codebook_dim == 8) ---------------------------------------------------------
+ * bc_vq_prepare_codebook: F.normalize(codebook) and its row sums of squares
+ *   (vq/factorized_vector_quantize.py:99,105).
+ * bc_vq_fwd: FactorizedVectorQuantize.forward in eval mode (factorized_vector_quantize.py:29-76):
+ *   z [B][D][T] -> in_proj (folded WN Linear, w_in [8][D], b_in [8]) -> decode_latents (:93-108) ->
+ *   idx [B][T] int64; z_e_out [B][8][T] (optional, may be NULL); post_out [B][D][T] = out_proj of
+ *   the straight-through z_q (optional, may be NULL; w_out [D][8], b_out [D]).
+ * bc_vq_argmin: decode_latents' search alone: z_e rows [N][8] -> idx [N] int64.  Given the same
+ *   z_e the indices equal the reference's ("VQ exactness").
+ * bc_vq2emb: FactorizedVectorQuantize.vq2emb (:78-81): idx[n*idx_stride] -> emb [N][D] (= (B,T,D)
+ *   as the reference returns); w_out == NULL means proj=False (emb = codebook rows, D == dim);
+ *   accumulate != 0 adds into emb (ResidualVQ.vq2emb sum, residual_vq.py:42-48).
+ * bc_rvq_update: ResidualVQ bookkeeping (residual_vq.py:31-33): residual -= q; out (+)= q. */
+int bc_vq_prepare_codebook(const float* codebook, float* codebook_norm, float* codebook_sq,
+                           int n_codes, int dim, void* stream);
+int bc_vq_fwd(const float* z, const float* w_in, const float* b_in, const float* codebook,
+              const float* codebook_norm, const float* codebook_sq, const float* w_out,
+              const float* b_out, long long* idx, float* z_e_out, float* post_out,
+              int B, int D, int T, int n_codes, int dim, void* stream);
+int bc_vq_argmin(const float* z_e, const float* codebook_norm, const float* codebook_sq,
+                 long long* idx, long long N, int n_codes, int dim, void* stream);
+int bc_vq2emb(const long long* idx, long long idx_stride, const float* codebook,
+              const float* w_out, const float* b_out, float* emb, long long N, int D, int n_codes,
+              int dim, int accumulate, void* stream);
+int bc_rvq_update(float* residual, float* out, const float* q, long long n, int first,
+                  void* stream);
+
+/* ---- Layout helpers & synthetic input --------------------------------------------------------
+ * bc_btc_to_ctb: x[B][C][T] -> y[C][T][B];  bc_ctb_to_btc_add: out = transpose(y) + skip.
+ * bc_synth_clips: x[B][T] white noise, clip i = clip0 + b (SURVEY.md §8(d) spec). */
+int bc_btc_to_ctb(const float* x, float* y, int B, int C, int T, void* stream);
+int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int C, int T,
+                      void* stream);
+int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BIGCODEC_H */

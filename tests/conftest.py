@@ -1,0 +1,48 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "reference: needs /root/reference (development container only)")
+
+
+def pytest_collection_modifyitems(config, items):
+    import torch
+
+    has_gpu = torch.cuda.is_available()
+    for item in items:
+        if "gpu" in item.keywords and not has_gpu:
+            item.add_marker(pytest.mark.skip(reason="no HIP device"))
+
+
+def load_golden(name):
+    d = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    out = {k: d[k] for k in d.files}
+    if "meta" in out:
+        out["meta"] = json.loads(str(out["meta"]))
+    return out
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden
+
+
+@pytest.fixture(scope="session")
+def dev():
+    import torch
+
+    from audiotokenization_amd import _lib
+
+    _lib.load()  # the HIP library must load: no fallback
+    return torch.device("cuda", 0)

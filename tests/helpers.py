@@ -1,0 +1,78 @@
+"""Shared test helpers: build models with the synthetic weight spec, oracle state dicts, tolerances."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from audiotokenization_amd import config as cfgmod
+from audiotokenization_amd import synth
+from audiotokenization_amd.codec import BigCodecDecoder, BigCodecEncoder
+
+
+def synth_load(module: torch.nn.Module, prefix: str, seed: int = 0) -> dict:
+    """Load the synthetic spec into `module` (keys prefixed like the Lightning module) and return
+    the module-level numpy state dict."""
+    sd = module.state_dict()
+    full = {prefix + k: v for k, v in sd.items()}
+    syn = synth.synth_state_dict(full, seed=seed)
+    local = {k[len(prefix):]: v for k, v in syn.items()}
+    module.load_state_dict({k: torch.from_numpy(v) for k, v in local.items()}, strict=True)
+    return local
+
+
+def build_models(name: str, device=None, **ov):
+    """(encoder, decoder, enc_sd, dec_sd, enc_cfg, dec_cfg) with synthetic weights."""
+    cfg = cfgmod.preset(name, **ov)
+    ek = cfgmod.encoder_kwargs(cfg.model.codec_encoder)
+    dk = cfgmod.decoder_kwargs(cfg.model.codec_decoder)
+    enc = BigCodecEncoder(**ek)
+    dec = BigCodecDecoder(**dk)
+    esd = synth_load(enc, "encoder.")
+    dsd = synth_load(dec, "decoder.")
+    enc.eval()
+    dec.eval()
+    if device is not None:
+        enc.to(device)
+        dec.to(device)
+    return enc, dec, esd, dsd, ek, dk
+
+
+def torch_sd(sd_np):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd_np.items()}
+
+
+def max_rel_err(a, b) -> float:
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    scale = b.abs().max().clamp_min(1e-30)
+    return float((a - b).abs().max() / scale)
+
+
+def assert_close_rel(a, b, tol: float, what: str = ""):
+    err = max_rel_err(a, b)
+    assert err <= tol, f"{what}: max |a-b| / max|b| = {err:.3e} > {tol:.1e}"
+
+
+def top2_gap(z_e: torch.Tensor, codebook: torch.Tensor) -> np.ndarray:
+    """fp64 gap between the best and the second-best VQ distance of every frame of z_e (B, 8, F)."""
+    b, d, t = z_e.shape
+    e = z_e.permute(0, 2, 1).reshape(-1, d).double()
+    e = e / e.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    c = codebook.double()
+    c = c / c.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    dist = (e * e).sum(1, keepdim=True) - 2 * e @ c.t() + (c * c).sum(1)[None]
+    v, _ = torch.topk(dist, 2, dim=1, largest=False)
+    return (v[:, 1] - v[:, 0]).reshape(b, t).float().numpy()
+
+
+def index_mismatches(got, want, gap, gap_tol: float = 1e-4):
+    """Compare indices; every mismatch must sit at a frame whose fp64 top-2 distance gap is below
+    gap_tol (a near-tie that legitimately flips under fp32 reassociation).  Returns (n_mismatch,
+    max gap among mismatches)."""
+    got = np.asarray(got).reshape(-1)
+    want = np.asarray(want).reshape(-1)
+    gap = np.asarray(gap).reshape(-1)
+    bad = np.nonzero(got != want)[0]
+    worst = float(gap[bad].max()) if bad.size else 0.0
+    assert worst <= gap_tol, f"{bad.size} index mismatches, one at a certified gap {worst:.3e} > {gap_tol:.1e}"
+    return bad.size, worst

@@ -1,0 +1,94 @@
+"""The CPU oracle (oracle/bigcodec_oracle.py, oracle/vq_oracle.c) reproduces the reference's own
+outputs (tests/golden/, produced from /root/reference by tools/make_golden.py) bit for bit."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import build_models, torch_sd
+from oracle import bigcodec_oracle as O
+from oracle import vq_c
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+MODEL_FILES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "model_*.npz")))
+LAYER_FILES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "layers_*.npz")))
+
+
+@pytest.mark.parametrize("fname", MODEL_FILES)
+def test_model_fixture(golden, fname):
+    g = golden(fname)
+    meta = g["meta"]
+    torch.set_num_threads(8)
+    _, _, esd, dsd, ek, dk = build_models(meta["model"], **meta["overrides"])
+    esd, dsd = torch_sd(esd), torch_sd(dsd)
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        lat = O.encoder_forward(x, esd, ek)
+        assert torch.equal(lat, torch.from_numpy(g["latent"]))
+        post, codes, losses = O.rvq_forward(lat, dsd, "quantizer.", dk["vq_num_quantizers"])
+        assert torch.equal(codes, torch.from_numpy(g["codes"]))
+        assert torch.equal(post, torch.from_numpy(g["post"]))
+        assert torch.equal(losses, torch.zeros(dk["vq_num_quantizers"]))
+        if "wav" in g:
+            wav = O.decoder_forward(post, dsd, dk)
+            assert torch.equal(wav, torch.from_numpy(g["wav"]))
+            emb = O.vq2emb(codes.permute(1, 2, 0), dsd, "quantizer.", dk["vq_num_quantizers"])
+            assert torch.equal(emb, torch.from_numpy(g["vq2emb"]))
+
+
+@pytest.mark.parametrize("fname", LAYER_FILES)
+def test_layer_fixture(golden, fname):
+    g = golden(fname)
+    meta = g["meta"]
+    _, _, esd, dsd, ek, dk = build_models(meta["model"], **meta["overrides"])
+    esd, dsd = torch_sd(esd), torch_sd(dsd)
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        lat = O.encoder_forward(x, esd, ek)
+        assert torch.equal(lat, torch.from_numpy(g[f"enc_{meta['n_enc'] - 1}"]))
+        post, _, _ = O.rvq_forward(lat, dsd)
+        wav = O.decoder_forward(post, dsd, dk)
+        assert torch.equal(wav, torch.from_numpy(g[f"dec_{meta['n_dec'] - 1}"]))
+
+
+def test_aa_fixture(golden):
+    from audiotokenization_amd.modules import UpSample1d, DownSample1d
+
+    g = golden("aa_activation.npz")
+    # the product's init-time Kaiser-sinc restatement equals the reference buffers
+    assert np.array_equal(UpSample1d(2, 12).filter.numpy(), g["up_filter"])
+    assert np.array_equal(DownSample1d(2, 12).lowpass.filter.numpy(), g["down_filter"])
+    fu, fd = torch.from_numpy(g["up_filter"]), torch.from_numpy(g["down_filter"])
+    for T in (1, 5, 37, 600):
+        sd = {"act.alpha": torch.from_numpy(g[f"alpha_{T}"]), "act.beta": torch.from_numpy(g[f"beta_{T}"]),
+              "upsample.filter": fu, "downsample.lowpass.filter": fd}
+        y = O.activation(torch.from_numpy(g[f"x_{T}"]), sd, "", True)
+        assert torch.equal(y, torch.from_numpy(g[f"y_{T}"])), T
+
+
+def test_vq_fixture_torch_oracle(golden):
+    g = golden("vq_decode_latents.npz")
+    z = torch.from_numpy(g["z_e"])
+    _, idx = O.decode_latents(z.t().reshape(1, 8, -1), torch.from_numpy(g["codebook"]))
+    assert torch.equal(idx.reshape(-1), torch.from_numpy(g["indices"]))
+
+
+def test_vq_fixture_c_oracle(golden):
+    g = golden("vq_decode_latents.npz")
+    idx = vq_c.argmin(g["z_e"], g["codebook"])
+    assert np.array_equal(idx, g["indices"])
+    # the planted exact tie resolves to the lower index, like torch's max()
+    assert idx[0] == 5
+
+
+def test_c_oracle_on_model_latents(golden):
+    """The C search reproduces the reference's end-to-end codes given the reference's z_e."""
+    for fname in MODEL_FILES:
+        g = golden(fname)
+        meta = g["meta"]
+        _, _, _, dsd, _, _ = build_models(meta["model"], **meta["overrides"])
+        ze = g["z_e"]  # (B, 8, F)
+        idx = vq_c.argmin(ze.transpose(0, 2, 1).reshape(-1, 8), dsd["quantizer.layers.0._codebook.weight"])
+        assert np.array_equal(idx, g["codes"][0].reshape(-1)), fname

@@ -1,0 +1,174 @@
+"""Generate tests/golden/*.npz from the REFERENCE modules (imported from /root/reference).
+
+Run in the development container only (the reference never travels):
+    python tools/make_golden.py
+Every fixture is data: synthetic inputs (audiotokenization_amd.synth spec) and the reference's
+outputs on them, plus metadata (torch version, shapes).  Weights are not stored: both sides
+synthesise them from the same counter-hash spec (synth.synth_state_dict).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+
+import refimport  # noqa: E402
+from audiotokenization_amd import config as cfgmod  # noqa: E402
+from audiotokenization_amd import synth  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def build_ref(ref, name, **ov):
+    cfg = cfgmod.preset(name, **ov)
+    ek = cfgmod.encoder_kwargs(cfg.model.codec_encoder)
+    dk = cfgmod.decoder_kwargs(cfg.model.codec_decoder)
+    enc = ref.encoder.BigCodecEncoder(**ek)
+    dec = ref.decoder.BigCodecDecoder(**dk)
+    for m, prefix in ((enc, "encoder."), (dec, "decoder.")):
+        sd = m.state_dict()
+        full = {prefix + k: v for k, v in sd.items()}
+        syn = synth.synth_state_dict(full, seed=0)
+        m.load_state_dict({k[len(prefix):]: torch.from_numpy(v) for k, v in syn.items()}, strict=True)
+        m.eval()
+    return enc, dec, ek, dk
+
+
+def top2_gap(z_e: torch.Tensor, codebook: torch.Tensor) -> np.ndarray:
+    """fp64 gap between the best and second-best distance per frame (the certificate used to judge
+    an index mismatch: a flip at a gap below the fp32 noise floor is not an error)."""
+    b, d, t = z_e.shape
+    e = z_e.permute(0, 2, 1).reshape(-1, d).double()
+    e = e / e.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    c = codebook.double()
+    c = c / c.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    dist = (e * e).sum(1, keepdim=True) - 2 * e @ c.t() + (c * c).sum(1)[None]
+    v, _ = torch.topk(dist, 2, dim=1, largest=False)
+    return (v[:, 1] - v[:, 0]).reshape(b, t).float().numpy()
+
+
+@torch.no_grad()
+def model_case(ref, name, n_clips, n_samples, decode=True, tag=None, **ov):
+    t0 = time.time()
+    enc, dec, ek, dk = build_ref(ref, name, **ov)
+    x = torch.from_numpy(synth.synth_clips(n_clips, n_samples, clip0=0)).unsqueeze(1)
+    emb = enc(x)
+    post, codes, loss = dec(emb, vq=True)
+    fvq = dec.quantizer.layers[0]
+    z_e = fvq.in_proj(emb.transpose(1, 2)).transpose(1, 2)
+    gap = top2_gap(z_e, fvq.codebook.weight)
+    out = dict(x=x.numpy(), latent=emb.numpy(), z_e=z_e.numpy(), post=post.numpy(),
+               codes=codes.numpy(), gap=gap)
+    if decode:
+        wav = dec(post, vq=False)
+        out["wav"] = wav.numpy()
+        # vq2emb path (codec_decoder.py:96-99) -> (B, F, D)
+        emb2 = dec.vq2emb(codes.permute(1, 2, 0))
+        out["vq2emb"] = emb2.numpy()
+    tag = tag or name + "".join(f"_{k}" for k, v in ov.items() if v)
+    meta = dict(model=name, overrides=ov, n_clips=n_clips, n_samples=n_samples, torch=torch.__version__,
+                encoder_kwargs=ek, decoder_kwargs=dk, seconds=round(time.time() - t0, 2))
+    np.savez_compressed(os.path.join(OUT, f"model_{tag}.npz"), meta=json.dumps(meta), **out)
+    print(f"model_{tag}: {meta['seconds']} s  codes {codes.shape}")
+
+
+@torch.no_grad()
+def layers_case(ref, name="base", n_samples=1600, **ov):
+    """Per-layer known answers for one short clip: output of every encoder stage and decoder stage."""
+    enc, dec, ek, dk = build_ref(ref, name, **ov)
+    x = torch.from_numpy(synth.synth_clips(1, n_samples, clip0=7)).unsqueeze(1)
+    out = {"x": x.numpy()}
+    h = x
+    for i, m in enumerate(enc.block):
+        h = m(h)
+        out[f"enc_{i}"] = h.numpy()
+    post, codes, _ = dec(h, vq=True)
+    h = post
+    for i, m in enumerate(dec.model):
+        h = m(h)
+        out[f"dec_{i}"] = h.numpy()
+    tag = name + "".join(f"_{k}" for k, v in ov.items() if v)
+    meta = dict(model=name, overrides=ov, n_samples=n_samples, torch=torch.__version__, n_enc=len(enc.block),
+                n_dec=len(dec.model))
+    np.savez_compressed(os.path.join(OUT, f"layers_{tag}.npz"), meta=json.dumps(meta), **out)
+    print(f"layers_{tag}")
+
+
+@torch.no_grad()
+def vq_case(ref):
+    """decode_latents known answers on random projected latents, including exact ties and
+    near-ties (duplicated / perturbed codebook rows) and zero / tiny rows."""
+    g = torch.Generator().manual_seed(1234)
+    fvq = ref.fvq.FactorizedVectorQuantize(dim=512, codebook_size=8192, codebook_dim=8, commitment=0.25)
+    cb = torch.rand(8192, 8, generator=g) * 2 - 1
+    cb[100] = cb[5]                       # exact duplicate: ties must resolve to the lower index 5
+    cb[4000] = cb[17] * 2.0               # same direction, different norm: normalized ties
+    cb[4001] = cb[18] * (1 + 2 ** -22)    # near-duplicate direction
+    fvq._codebook.weight.copy_(cb)
+    n = 6000
+    z = torch.randn(n, 8, generator=g) * torch.exp(torch.randn(n, 1, generator=g))
+    z[0] = cb[5]
+    z[1] = cb[17]
+    z[2] = cb[18]
+    z[3] = 0.0                            # zero row: normalize -> 0, all distances equal -> index 0
+    z[4] = 1e-30                          # tiny row (eps clamp)
+    z[5] = cb[5] * 1e3
+    lat = z.t().reshape(1, 8, n)          # (b, d, t) with b = 1
+    z_q, idx = fvq.decode_latents(lat)
+    np.savez_compressed(os.path.join(OUT, "vq_decode_latents.npz"), z_e=z.numpy(), codebook=cb.numpy(),
+                        indices=idx.reshape(-1).numpy(), meta=json.dumps(dict(torch=torch.__version__, n=n)))
+    print("vq_decode_latents", n)
+
+
+@torch.no_grad()
+def aa_case(ref):
+    """Anti-aliased Activation1d known answers (act.py:25-32), incl. short rows (T < taps)."""
+    g = torch.Generator().manual_seed(99)
+    out = {}
+    for T in (1, 5, 37, 600):
+        act = ref.alias_free.Activation1d(activation=ref.activations.SnakeBeta(6, alpha_logscale=True),
+                                          antialias=True)
+        act.act.alpha.copy_(torch.rand(6, generator=g) - 0.5)
+        act.act.beta.copy_(torch.rand(6, generator=g) - 0.5)
+        x = torch.randn(2, 6, T, generator=g)
+        out[f"x_{T}"] = x.numpy()
+        out[f"alpha_{T}"] = act.act.alpha.numpy()
+        out[f"beta_{T}"] = act.act.beta.numpy()
+        out[f"y_{T}"] = act(x).numpy()
+    out["up_filter"] = act.upsample.filter.numpy()
+    out["down_filter"] = act.downsample.lowpass.filter.numpy()
+    np.savez_compressed(os.path.join(OUT, "aa_activation.npz"), meta=json.dumps(dict(torch=torch.__version__)), **out)
+    print("aa_activation")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(8)
+    ref = refimport.load()
+    vq_case(ref)
+    aa_case(ref)
+    layers_case(ref, "base")
+    layers_case(ref, "debug", n_samples=1600)
+    layers_case(ref, "base", n_samples=1600, causal=True)
+    layers_case(ref, "base", n_samples=800, antialias=True)
+    model_case(ref, "debug", 2, 24000)
+    model_case(ref, "base", 2, 24000)
+    model_case(ref, "default", 1, 24000)
+    model_case(ref, "base", 1, 8000, causal=True)
+    model_case(ref, "debug", 1, 4800, antialias=True)
+    # config 1: 1 x 1 s clip, inference_full pad quirk (+200 -> 24200 samples)
+    model_case(ref, "default", 1, 24200, tag="config1_default")
+
+
+if __name__ == "__main__":
+    main()
