@@ -58,10 +58,12 @@ def top2_gap(z_e: torch.Tensor, codebook: torch.Tensor) -> np.ndarray:
 
 
 @torch.no_grad()
-def model_case(ref, name, n_clips, n_samples, decode=True, tag=None, **ov):
+def model_case(ref, name, n_clips, n_samples, decode=True, tag=None, hop_pad=None, **ov):
     t0 = time.time()
     enc, dec, ek, dk = build_ref(ref, name, **ov)
     x = torch.from_numpy(synth.synth_clips(n_clips, n_samples, clip0=0)).unsqueeze(1)
+    if hop_pad:  # inference_full.py:712: F.pad(x, (0, hop - T % hop)), a full hop on a multiple
+        x = F.pad(x, (0, hop_pad - (x.shape[2] % hop_pad)))
     emb = enc(x)
     post, codes, loss = dec(emb, vq=True)
     fvq = dec.quantizer.layers[0]
@@ -167,7 +169,7 @@ def main():
     model_case(ref, "base", 1, 8000, causal=True)
     model_case(ref, "debug", 1, 4800, antialias=True)
     # config 1: 1 x 1 s clip, inference_full pad quirk (+200 -> 24200 samples)
-    model_case(ref, "default", 1, 24200, tag="config1_default")
+    model_case(ref, "default", 1, 24000, tag="config1_default", hop_pad=200)
 
 
 if __name__ == "__main__":
