@@ -8,8 +8,9 @@ from . import _lib  # noqa: F401
 from .codec import BigCodecDecoder, BigCodecEncoder
 from .config import AttrDict, load_config, preset
 from .lightning_shim import CodecLightningModule
-from .modules import (Activation1d, DecoderBlock, EncoderBlock, FactorizedVectorQuantize, ResidualUnit,
-                      ResidualVQ, ResLSTM, SnakeBeta)
+from .blocks import DecoderBlock, EncoderBlock, ResidualUnit, ResLSTM
+from .conv import WNConv1d, WNConvTranspose1d
+from .modules import Activation1d, FactorizedVectorQuantize, ResidualVQ, SnakeBeta
 
 __all__ = [
     "BigCodecEncoder", "BigCodecDecoder", "CodecLightningModule", "AttrDict", "load_config", "preset",

@@ -22,18 +22,18 @@ L = C.c_longlong
 # name -> (restype, argtypes)
 _SIGS = {
     "bc_abi_version": (I, []),
-    "bc_conv1d_select_cfg": (I, [I, I]),
+    "bc_conv1d_select_cfg": (I, [I, I, I, I, I]),
     "bc_conv1d_packed_floats": (L, [I, I, I, I]),
     "bc_conv1d_pack": (I, [P, P, I, I, I, I]),
-    "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
     "bc_convT1d_phase_taps": (I, [I, I]),
-    "bc_convT1d_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
+    "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
     "bc_aa_snake_fwd": (I, [P, P, P, P, P, P, I, I, I, P]),
     "bc_lstm_hh_packed_floats": (L, [I]),
     "bc_lstm_pack_hh": (I, [P, P, I]),
     "bc_lstm_workspace_floats": (L, [I, I, I]),
-    "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P]),
+    "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
     "bc_vq_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P]),
     "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
@@ -44,6 +44,7 @@ _SIGS = {
     "bc_synth_clips": (I, [P, I, L, L, P]),
 }
 EXPORTED = tuple(_SIGS)
+ABI_VERSION = 2  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -158,14 +159,15 @@ def active_timer() -> KernelTimer | None:
     return _timer
 
 
-# conv tile configs (csrc/conv1d.hip kCfgs) -> template arguments, for kernel-symbol naming
-CONV_CFGS = {0: (4, 2, 4, 2, 8), 1: (4, 1, 4, 4, 8), 2: (3, 1, 4, 4, 8), 3: (2, 1, 4, 4, 8), 4: (1, 1, 4, 4, 8),
-             5: (4, 2, 4, 2, 4), 6: (4, 1, 4, 4, 4), 7: (3, 1, 4, 4, 4), 8: (2, 1, 4, 4, 4), 9: (1, 1, 4, 4, 4)}
+# conv tile configs (csrc/conv1d.hip kTiles x kBKC, cfg = tile*4 + bkc_index) -> template arguments
+_TILES = [(4, 2, 4, 2), (4, 1, 4, 4), (3, 1, 4, 4), (2, 1, 4, 4), (1, 1, 4, 4)]
+_BKC = [32, 16, 8, 4]
+CONV_CFGS = {t * 4 + b: _TILES[t] + (_BKC[b],) for t in range(5) for b in range(4)}
 
 
-def conv_kernel_name(cfg: int, snake: bool) -> str:
+def conv_kernel_name(cfg: int) -> str:
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
-    return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}, {'true' if snake else 'false'}>"
+    return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
 
 
 def ptr_array(ptrs):

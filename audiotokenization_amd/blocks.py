@@ -1,0 +1,245 @@
+"""Composite blocks of the BigCodec stacks (vq/module.py:74-167) and the fused data flow.
+
+Every conv in the reference is preceded by an Activation1d (Snake).  The HIP path computes each
+Snake once, in the epilogue of the kernel that PRODUCES its input; a producer whose raw output is
+still needed (as a ResidualUnit skip input) writes both raw and activated tensors.  The flow is
+expressed with producer functions that take
+
+    want_raw : does any consumer still need the raw output?
+    next_act : the Activation1d that consumes the output (None: raw output only)
+
+and return (raw or None, activated or None).  Anti-aliased activations (bc_aa_snake_fwd) cannot be
+an epilogue; they run as their own kernel on the raw output.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn import Parameter
+
+from . import _lib as L
+from .conv import WNConv1d, WNConvTranspose1d
+from .modules import Activation1d, SnakeBeta, _DeviceCache, _as_input, _cpu, _pkey
+
+__all__ = ["ResidualUnit", "EncoderBlock", "DecoderBlock", "LSTM", "ResLSTM"]
+
+Flow = Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]
+
+
+def _fusable(act: Optional[Activation1d]) -> bool:
+    return act is not None and not act.antialias
+
+
+def produce_conv(conv, inp, residual=None, want_raw=True, next_act: Optional[Activation1d] = None,
+                 epilogue: int = 0) -> Flow:
+    """Run `conv` on an already-activated input and hand its output to `next_act`'s consumer."""
+    if next_act is None:
+        return conv.run(inp, residual, epilogue), None
+    if _fusable(next_act):
+        co = next_act.act.coeffs(inp.device)
+        if want_raw:
+            y, ya = conv.run(inp, residual, epilogue, out_snake=co, dual=True)
+            return y, ya
+        return None, conv.run(inp, residual, epilogue, out_snake=co)
+    y = conv.run(inp, residual, epilogue)
+    return y, next_act(y)
+
+
+def produce_convT(conv, inp, want_raw=True, next_act: Optional[Activation1d] = None) -> Flow:
+    if next_act is None:
+        return conv.run(inp), None
+    if _fusable(next_act):
+        co = next_act.act.coeffs(inp.device)
+        if want_raw:
+            return conv.run(inp, out_snake=co, dual=True)
+        return None, conv.run(inp, out_snake=co)
+    y = conv.run(inp)
+    return y, next_act(y)
+
+
+class ResidualUnit(nn.Module):
+    """vq/module.py:74-89: x + conv1(act2(conv7_d(act1(x)))).  Two launches: conv7 (epilogue =
+    act2), conv1 (epilogue = skip add [+ the next block's Snake])."""
+
+    def __init__(self, dim: int = 16, dilation: int = 1, causal: bool = False, antialias: bool = False):
+        super().__init__()
+        pad = 0 if causal else ((7 - 1) * dilation) // 2
+        self.block = nn.Sequential(
+            Activation1d(activation=SnakeBeta(dim, alpha_logscale=True), antialias=antialias),
+            WNConv1d(dim, dim, kernel_size=7, dilation=dilation, padding=pad, causal=causal),
+            Activation1d(activation=SnakeBeta(dim, alpha_logscale=True), antialias=antialias),
+            WNConv1d(dim, dim, kernel_size=1),
+        )
+
+    @property
+    def first_act(self) -> Activation1d:
+        return self.block[0]
+
+    def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
+        """x_act = self.first_act(x_raw) (computed by the producer)."""
+        _, h = produce_conv(self.block[1], x_act, None, want_raw=False, next_act=self.block[2])
+        return produce_conv(self.block[3], h, residual=x_raw, want_raw=want_raw, next_act=next_act)
+
+    def forward(self, x):
+        x = _as_input(x)
+        return self.flow(x, self.first_act(x))[0]
+
+
+class EncoderBlock(nn.Module):
+    """vq/module.py:91-113: ResidualUnits -> Activation1d -> strided conv (k=2s) C/2 -> C."""
+
+    def __init__(self, dim: int = 16, stride: int = 1, dilations=(1, 3, 9), causal: bool = False,
+                 antialias: bool = False):
+        super().__init__()
+        runits = [ResidualUnit(dim // 2, dilation=d, causal=causal, antialias=antialias) for d in dilations]
+        pad = 0 if causal else (stride // 2 + stride % 2 if stride != 1 else 0)
+        self.block = nn.Sequential(
+            *runits,
+            Activation1d(activation=SnakeBeta(dim // 2, alpha_logscale=True), antialias=antialias),
+            WNConv1d(dim // 2, dim, kernel_size=2 * stride if stride != 1 else 1, stride=stride, padding=pad,
+                     causal=causal),
+        )
+
+    @property
+    def first_act(self) -> Activation1d:
+        return self.block[0].first_act
+
+    def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
+        n = len(self.block)
+        rus = [self.block[i] for i in range(n - 2)]
+        for i, ru in enumerate(rus):
+            last = i == len(rus) - 1
+            nxt = self.block[n - 2] if last else rus[i + 1].first_act
+            x_raw, x_act = ru.flow(x_raw, x_act, want_raw=not last, next_act=nxt)
+        return produce_conv(self.block[n - 1], x_act, None, want_raw=want_raw, next_act=next_act)
+
+    def forward(self, x):
+        x = _as_input(x)
+        return self.flow(x, self.first_act(x))[0]
+
+
+class DecoderBlock(nn.Module):
+    """vq/module.py:115-141: Activation1d -> transposed conv (k=2s) -> ResidualUnits."""
+
+    def __init__(self, input_dim: int = 16, output_dim: int = 8, stride: int = 1, dilations=(1, 3, 9),
+                 causal: bool = False, antialias: bool = False):
+        super().__init__()
+        if causal:
+            tconv_kwargs = {}
+        else:
+            tconv_kwargs = {"padding": stride // 2 + stride % 2 if stride != 1 else 0,
+                            "output_padding": stride % 2 if stride != 1 else 0}
+        self.block = nn.Sequential(
+            Activation1d(activation=SnakeBeta(input_dim, alpha_logscale=True), antialias=antialias),
+            WNConvTranspose1d(input_dim, output_dim, kernel_size=2 * stride if stride != 1 else 1, stride=stride,
+                              causal=causal, **tconv_kwargs),
+        )
+        self.block.extend([ResidualUnit(output_dim, dilation=d, causal=causal, antialias=antialias)
+                           for d in dilations])
+
+    @property
+    def first_act(self) -> Activation1d:
+        return self.block[0]
+
+    def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
+        rus = [self.block[i] for i in range(2, len(self.block))]
+        y_raw, y_act = produce_convT(self.block[1], x_act, want_raw=True,
+                                     next_act=rus[0].first_act if rus else next_act)
+        for i, ru in enumerate(rus):
+            last = i == len(rus) - 1
+            y_raw, y_act = ru.flow(y_raw, y_act, want_raw=(want_raw if last else True),
+                                   next_act=next_act if last else rus[i + 1].first_act)
+        return y_raw, y_act
+
+    def forward(self, x):
+        x = _as_input(x)
+        return self.flow(x, self.first_act(x))[0]
+
+
+class LSTM(nn.Module):
+    """Parameter container with torch.nn.LSTM's names (weight_ih_l{k}, weight_hh_l{k}, bias_ih_l{k},
+    bias_hh_l{k}; batch_first) so reference checkpoints load; the recurrence runs in
+    bc_reslstm_fwd."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1, bias=True, batch_first=True, dropout=0.0,
+                 bidirectional=False):
+        super().__init__()
+        if bidirectional:
+            raise NotImplementedError("bidirectional ResLSTM is not used by any shipped config")
+        if not bias or not batch_first or dropout:
+            raise NotImplementedError("only bias=True, batch_first=True, dropout=0")
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.batch_first, self.bidirectional = batch_first, bidirectional
+        ref = nn.LSTM(input_size, hidden_size, num_layers, batch_first=True)  # torch's default init
+        for name, p in ref.named_parameters():
+            setattr(self, name, Parameter(p.detach().clone()))
+        self._cache = _DeviceCache()
+
+    def _plist(self):
+        out = []
+        for l in range(self.num_layers):
+            out += [getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"),
+                    getattr(self, f"bias_ih_l{l}"), getattr(self, f"bias_hh_l{l}")]
+        return out
+
+    def prepared(self, device):
+        def build():
+            lib = L.load()
+            H = self.hidden_size
+            if self.input_size != H:
+                raise NotImplementedError("ResLSTM requires input_size == hidden_size")
+            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1)
+            wih, whh, bias = [], [], []
+            for l in range(self.num_layers):
+                w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
+                packed = np.empty(lib.bc_conv1d_packed_floats(4 * H, H, 1, cfg), dtype=np.float32)
+                L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
+                wih.append(torch.from_numpy(packed).to(device))
+                w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
+                packed = np.empty(lib.bc_lstm_hh_packed_floats(H), dtype=np.float32)
+                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H)
+                whh.append(torch.from_numpy(packed).to(device))
+                b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
+                bias.append(b.contiguous().to(device))
+            arrs = (L.ptr_array([t.data_ptr() for t in wih]), L.ptr_array([t.data_ptr() for t in bias]),
+                    L.ptr_array([t.data_ptr() for t in whh]))
+            return (wih, whh, bias), arrs
+        return self._cache.get(_pkey(*self._plist()) + (str(device),), build)
+
+
+class ResLSTM(nn.Module):
+    """vq/module.py:143-167: y = LSTM(x^T)^T + x for x (B, F, T)."""
+
+    def __init__(self, dimension: int, num_layers: int = 2, bidirectional: bool = False, skip: bool = True):
+        super().__init__()
+        if not skip:
+            raise NotImplementedError("ResLSTM(skip=False) is not used by the reference models")
+        self.skip = skip
+        self.lstm = LSTM(dimension, dimension if not bidirectional else dimension // 2, num_layers,
+                         batch_first=True, bidirectional=bidirectional)
+
+    def run(self, x, out_snake=None):
+        x = _as_input(x)
+        B, H, T = x.shape
+        _, (pwih, pbias, pwhh) = self.lstm.prepared(x.device)
+        lib = L.load()
+        ws = torch.empty(int(lib.bc_lstm_workspace_floats(B, H, T)), device=x.device, dtype=torch.float32)
+        y = torch.empty_like(x)
+        sa, sb = out_snake if out_snake is not None else (None, None)
+        L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
+               L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.stream_of(x))
+        return y
+
+    def flow(self, x_raw, want_raw=True, next_act=None) -> Flow:
+        if next_act is None:
+            return self.run(x_raw), None
+        if _fusable(next_act) and not want_raw:
+            return None, self.run(x_raw, out_snake=next_act.act.coeffs(x_raw.device))
+        y = self.run(x_raw)
+        return y, next_act(y)
+
+    def forward(self, x):
+        return self.run(x)

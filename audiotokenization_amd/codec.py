@@ -1,22 +1,25 @@
 """BigCodecEncoder / BigCodecDecoder (vq/codec_encoder.py:14-90, vq/codec_decoder.py:15-142) on the
-HIP kernels, with the reference's constructor signatures, state_dict keys and call surface."""
+HIP kernels, with the reference's constructor signatures, state_dict keys and call surface.
+
+forward() runs the whole stack as one fused flow (blocks.py): every Snake is computed once in
+the epilogue of the kernel producing its input, the ResLSTM writes the final Snake directly, and
+the decoder's tanh is the last conv's epilogue."""
 from __future__ import annotations
 
 import numpy as np
 import torch
 import torch.nn as nn
 
-from . import _lib as L
-from .modules import (Activation1d, DecoderBlock, EncoderBlock, ResidualVQ, ResLSTM, SnakeBeta, WNConv1d,
-                      _as_input, run_activation_then)
+from .blocks import DecoderBlock, EncoderBlock, ResLSTM, produce_conv
+from .conv import WNConv1d
+from .modules import Activation1d, ResidualVQ, SnakeBeta, _as_input
 
 
 class _Tanh(nn.Module):
-    """nn.Tanh position holder in the decoder Sequential; the tanh is fused into the last conv's
-    epilogue (bc_conv1d_fwd epilogue=1) when the decoder runs as a whole."""
+    """nn.Tanh position holder (codec_decoder.py:80); it runs fused in the last conv's epilogue."""
 
-    def forward(self, x):  # standalone use of decoder.model[-1] is not a hot path
-        raise NotImplementedError("the decoder's final tanh runs fused in the last conv")
+    def forward(self, x):
+        raise NotImplementedError("the decoder's final tanh runs fused in the last conv's epilogue")
 
 
 class BigCodecEncoder(nn.Module):
@@ -46,19 +49,31 @@ class BigCodecEncoder(nn.Module):
 
     def forward(self, x):
         x = _as_input(x)
-        blk = self.block
-        n = len(blk)
-        for i in range(n - 2):
-            x = blk[i](x)
-        h, co = run_activation_then(blk[n - 2], x)
-        return blk[n - 1].run(h, snake=co)
+        blk = list(self.block)
+        final_act, last_conv = blk[-2], blk[-1]
+        stages = blk[1:-2]  # EncoderBlocks [+ ResLSTM]
+        # consumer activation of each stage's output
+        def next_act_of(i):
+            if i + 1 < len(stages):
+                nxt = stages[i + 1]
+                return nxt.first_act if isinstance(nxt, EncoderBlock) else None  # ResLSTM takes raw
+            return final_act
+        y, ya = produce_conv(blk[0], x, None, want_raw=True, next_act=next_act_of(-1) if stages else final_act)
+        for i, st in enumerate(stages):
+            nact = next_act_of(i)
+            want_raw = i + 1 < len(stages)  # the next stage needs the raw tensor (RU skip / LSTM input)
+            if isinstance(st, EncoderBlock):
+                y, ya = st.flow(y, ya, want_raw=want_raw, next_act=nact)
+            else:
+                y, ya = st.flow(y, want_raw=want_raw, next_act=nact)
+        return produce_conv(last_conv, ya, None, want_raw=True, next_act=None)[0]
 
     def inference(self, x):
         return self.forward(x)
 
     def remove_weight_norm(self):
         for m in self.modules():
-            if hasattr(m, "remove_weight_norm") and m is not self and "weight_v" in m._parameters:
+            if m is not self and "weight_v" in m._parameters and hasattr(m, "remove_weight_norm"):
                 m.remove_weight_norm()
 
 
@@ -79,9 +94,8 @@ class BigCodecDecoder(nn.Module):
         if fsq:
             raise NotImplementedError("FSQ quantizer (fsq=True) is a SURVEY §8(f) 'next' item; no shipped "
                                       "config enables it")
-        self.quantizer = ResidualVQ(num_quantizers=vq_num_quantizers, dim=in_channels,
-                                    codebook_size=codebook_size, codebook_dim=codebook_dim,
-                                    threshold_ema_dead_code=2, commitment=vq_commit_weight,
+        self.quantizer = ResidualVQ(num_quantizers=vq_num_quantizers, dim=in_channels, codebook_size=codebook_size,
+                                    codebook_dim=codebook_dim, threshold_ema_dead_code=2, commitment=vq_commit_weight,
                                     weight_init=vq_weight_init, full_commit_loss=vq_full_commit_loss)
         channels = upsample_initial_channel
         layers = [WNConv1d(in_channels, channels, kernel_size=7, padding=3, causal=causal)]
@@ -100,14 +114,28 @@ class BigCodecDecoder(nn.Module):
         self.model = nn.Sequential(*layers)
 
     def decode(self, x):
-        """self.model(x) with the final Snake and tanh fused into the last conv."""
+        """self.model(x): fused flow; final Snake in the producer of the last conv's input, tanh in
+        the last conv's epilogue."""
         x = _as_input(x)
-        m = self.model
-        n = len(m)
-        for i in range(n - 3):
-            x = m[i](x)
-        h, co = run_activation_then(m[n - 3], x)
-        return m[n - 2].run(h, snake=co, epilogue=1)
+        m = list(self.model)
+        final_act, last_conv = m[-3], m[-2]
+        stages = m[1:-3]  # [ResLSTM] + DecoderBlocks
+
+        def next_act_of(i):
+            if i + 1 < len(stages):
+                nxt = stages[i + 1]
+                return nxt.first_act if isinstance(nxt, DecoderBlock) else None
+            return final_act
+        first_next = next_act_of(-1) if stages else final_act
+        y, ya = produce_conv(m[0], x, None, want_raw=first_next is None, next_act=first_next)
+        for i, st in enumerate(stages):
+            nact = next_act_of(i)
+            want_raw = nact is None
+            if isinstance(st, DecoderBlock):
+                y, ya = st.flow(y, ya, want_raw=want_raw, next_act=nact)
+            else:
+                y, ya = st.flow(y, want_raw=want_raw, next_act=nact)
+        return produce_conv(last_conv, ya, None, want_raw=True, next_act=None, epilogue=1)[0]
 
     def forward(self, x, vq=True):
         if vq is True:
@@ -134,5 +162,5 @@ class BigCodecDecoder(nn.Module):
 
     def remove_weight_norm(self):
         for m in self.modules():
-            if hasattr(m, "remove_weight_norm") and m is not self and "weight_v" in m._parameters:
+            if m is not self and "weight_v" in m._parameters and hasattr(m, "remove_weight_norm"):
                 m.remove_weight_norm()

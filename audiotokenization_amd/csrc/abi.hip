@@ -11,37 +11,39 @@ extern "C" {
 
 int bc_abi_version(void) { return BC_ABI_VERSION; }
 
-int bc_conv1d_select_cfg(int Cout, int Cin) {
-  if (Cout <= 0 || Cin <= 0) return -1;
-  return conv_select_cfg(Cout, Cin);
+int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation) {
+  if (Cout <= 0 || Cin <= 0 || K <= 0 || stride <= 0 || dilation <= 0) return -1;
+  return conv_select_cfg(Cout, Cin, K, stride, dilation);
 }
 
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg) {
-  if (Cout <= 0 || Cin <= 0 || K <= 0 || cfg < 0 || cfg > 9) return -1;
+  if (Cout <= 0 || Cin <= 0 || K <= 0 || !conv_cfg_valid(cfg)) return -1;
   return conv_packed_floats(Cout, Cin, K, cfg);
 }
 
 int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg) {
-  if (!w_host || !packed_host || Cout <= 0 || Cin <= 0 || K <= 0 || cfg < 0 || cfg > 9)
+  if (!w_host || !packed_host || Cout <= 0 || Cin <= 0 || K <= 0 || !conv_cfg_valid(cfg))
     return BC_ERR_ARG;
   conv_pack_weight(w_host, packed_host, Cout, Cin, K, cfg);
   return BC_OK;
 }
 
-int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias,
-                  const float* snake_alpha_exp, const float* snake_inv_beta, const float* residual,
-                  float* y, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, const float* residual,
+                  const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
+                  float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
                   int dilation, int pad_left, int epilogue, int cfg, void* stream) {
   if (!x || !w_packed || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 ||
-      stride <= 0 || dilation <= 0 || pad_left < 0 || cfg < 0 || cfg > 9)
+      stride <= 0 || dilation <= 0 || pad_left < 0 || !conv_cfg_valid(cfg))
     return BC_ERR_ARG;
-  if ((snake_alpha_exp == nullptr) != (snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
   if (epilogue != 0 && epilogue != 1) return BC_ERR_ARG;
-  if (cfg != conv_select_cfg(Cout, Cin)) return BC_ERR_ARG;
+  if (epilogue == 1 && out_snake_alpha_exp) return BC_ERR_ARG;
+  if (cfg != conv_select_cfg(Cout, Cin, K, stride, dilation)) return BC_ERR_ARG;
   if (B == 0 || Tout == 0) return BC_OK;
   ConvArgs a{};
-  a.x = x; a.w = w_packed; a.bias = bias; a.sa = snake_alpha_exp; a.sb = snake_inv_beta;
-  a.res = residual; a.y = y;
+  a.x = x; a.w = w_packed; a.bias = bias; a.res = residual;
+  a.osa = out_snake_alpha_exp; a.osb = out_snake_inv_beta; a.y = y; a.y2 = y2;
   a.xbs = (long long)Cin * Tin; a.ybs = (long long)Cout * Tout; a.rbs = a.ybs;
   a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = Tout;
   a.K = K; a.s = stride; a.d = dilation; a.pl = pad_left;
@@ -55,17 +57,18 @@ int bc_convT1d_phase_taps(int K, int stride) {
 }
 
 int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bias,
-                   const float* snake_alpha_exp, const float* snake_inv_beta, float* y, int B,
-                   int Cin, int Tin, int Cout, int Tout, int K, int stride, int padding, int cfg,
-                   void* stream) {
+                   const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
+                   float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+                   int padding, int cfg, void* stream) {
   if (!x || !w_phases || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 ||
-      stride <= 0 || padding < 0 || cfg < 0 || cfg > 9)
+      stride <= 0 || padding < 0 || !conv_cfg_valid(cfg))
     return BC_ERR_ARG;
-  if ((snake_alpha_exp == nullptr) != (snake_inv_beta == nullptr)) return BC_ERR_ARG;
-  if (cfg != conv_select_cfg(Cout, Cin)) return BC_ERR_ARG;
-  if (B == 0 || Tout == 0) return BC_OK;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
   const int s = stride, p = padding;
   const int Kp = (K + s - 1) / s;  // taps per phase
+  if (cfg != conv_select_cfg(Cout, Cin, Kp, 1, 1)) return BC_ERR_ARG;
+  if (B == 0 || Tout == 0) return BC_OK;
   for (int r = 0; r < s; ++r) {
     if (!w_phases[r]) return BC_ERR_ARG;
     // outputs t = s*q - p + r, q in [q_lo, q_hi]
@@ -75,8 +78,8 @@ int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bi
     const int nout = q_hi - q_lo + 1;
     if (nout <= 0) continue;
     ConvArgs a{};
-    a.x = x; a.w = w_phases[r]; a.bias = bias; a.sa = snake_alpha_exp; a.sb = snake_inv_beta;
-    a.res = nullptr; a.y = y;
+    a.x = x; a.w = w_phases[r]; a.bias = bias; a.res = nullptr;
+    a.osa = out_snake_alpha_exp; a.osb = out_snake_inv_beta; a.y = y; a.y2 = y2;
     a.xbs = (long long)Cin * Tin; a.ybs = (long long)Cout * Tout; a.rbs = 0;
     a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = nout;
     // Kp-tap conv: tap j' reads input q - (Kp-1) + j' (weight W[ci][co][r + s*(Kp-1-j')]);
@@ -113,23 +116,30 @@ long long bc_lstm_hh_packed_floats(int H) {
 
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H) {
   if (!w_hh_host || !packed_host || H <= 0 || H % 16) return BC_ERR_ARG;
-  lstm_pack_hh(w_hh_host, packed_host, H);
+  if (lstm_fast_ok(H))
+    lstm_pack_hh2(w_hh_host, packed_host, H);  // layout of the register-resident fast step kernel
+  else
+    lstm_pack_hh(w_hh_host, packed_host, H);
   return BC_OK;
 }
 
-// workspace: xt [H][T*B] | gx [4H][T*B] | y0 [H][T*B] | y1 [H][T*B] | c [H][B]
+// workspace: xt [H][T*B] | gx [4H][T*B] | y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2
+static long long lstm_frag_floats(int B, int H) { return (long long)((B + 63) / 64) * 64 * H; }
+
 long long bc_lstm_workspace_floats(int B, int H, int T) {
   if (B < 0 || H <= 0 || T < 0) return -1;
   const long long tb = (long long)T * B;
-  return tb * H * 3 + tb * 4 * H + (long long)H * B;
+  return tb * H * 3 + tb * 4 * H + (long long)H * B + 2 * lstm_frag_floats(B, H);
 }
 
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
-                   const float* const* w_hh_packed, float* workspace, void* stream) {
+                   const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                   const float* out_snake_inv_beta, float* workspace, void* stream) {
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
       H % 16 || T < 0 || num_layers <= 0)
     return BC_ERR_ARG;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   hipStream_t st = S(stream);
   const long long tb = (long long)T * B;
@@ -139,16 +149,18 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
   float* ya = gx + tb * 4 * H;
   float* yb = ya + tb * H;
   float* cst = yb + tb * H;
+  float* frag[2] = {cst + (long long)H * B, cst + (long long)H * B + lstm_frag_floats(B, H)};
+  const bool fast = lstm_fast_ok(H);
   int rc = btc_to_ctb_launch(x, xt, B, H, T, st);
   if (rc) return rc;
-  const int cfg = conv_select_cfg(4 * H, H);
+  const int cfg = conv_select_cfg(4 * H, H, 1, 1, 1);
   const float* lin = xt;
   float* lout = ya;
   for (int l = 0; l < num_layers; ++l) {
     if (!w_ih_packed[l] || !w_hh_packed[l] || !bias[l]) return BC_ERR_ARG;
     ConvArgs a{};
-    a.x = lin; a.w = w_ih_packed[l]; a.bias = bias[l]; a.sa = nullptr; a.sb = nullptr;
-    a.res = nullptr; a.y = gx;
+    a.x = lin; a.w = w_ih_packed[l]; a.bias = bias[l]; a.res = nullptr;
+    a.osa = nullptr; a.osb = nullptr; a.y = gx; a.y2 = nullptr;
     a.xbs = 0; a.ybs = 0; a.rbs = 0;
     a.Cin = H; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
     a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
@@ -156,13 +168,15 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
     rc = conv_launch(a, 1, cfg, st);
     if (rc) return rc;
     for (int t = 0; t < T; ++t) {
-      rc = lstm_step_launch(gx, w_hh_packed[l], lout, cst, H, B, T, t, st);
+      rc = fast ? lstm_step_frag_launch(gx, w_hh_packed[l], frag[(t + 1) & 1], frag[t & 1], lout, cst,
+                                        H, B, T, t, st)
+                : lstm_step_launch(gx, w_hh_packed[l], lout, cst, H, B, T, t, st);
       if (rc) return rc;
     }
     lin = lout;
     lout = (lout == ya) ? yb : ya;
   }
-  return ctb_to_btc_add_launch(lin, x, out, B, H, T, st);
+  return ctb_to_btc_add_launch(lin, x, out_snake_alpha_exp, out_snake_inv_beta, out, B, H, T, st);
 }
 
 int bc_vq_prepare_codebook(const float* codebook, float* codebook_norm, float* codebook_sq,
@@ -217,7 +231,7 @@ int bc_btc_to_ctb(const float* x, float* y, int B, int C, int T, void* stream) {
 int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int C, int T,
                       void* stream) {
   if (!y || !skip || !out || B < 0 || C < 0 || T < 0) return BC_ERR_ARG;
-  return ctb_to_btc_add_launch(y, skip, out, B, C, T, S(stream));
+  return ctb_to_btc_add_launch(y, skip, nullptr, nullptr, out, B, C, T, S(stream));
 }
 
 int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream) {

@@ -4,22 +4,26 @@
 
 namespace bc {
 struct ConvArgs {
-  const float* x;
-  const float* w;
-  const float* bias;
-  const float* sa;
-  const float* sb;
-  const float* res;
-  float* y;
+  const float* x;      // input [B][Cin][Tin] (already activated: the Snake runs in the producer)
+  const float* w;      // packed folded weights
+  const float* bias;   // [Cout] or nullptr
+  const float* res;    // residual, same indexing as y, or nullptr
+  const float* osa;    // epilogue Snake alpha_exp [Cout] or nullptr
+  const float* osb;    // epilogue Snake inv_beta [Cout]
+  float* y;            // output (raw, or snake'd when osa != nullptr and y2 == nullptr)
+  float* y2;           // optional second output = snake(raw) (dual epilogue)
   long long xbs, ybs, rbs;
   int Cin, Tin, Cout, Nout;
   int K, s, d, pl;
   int yT, ostride, ooff;
-  int epi;
-  int nchunks, win;
+  int epi;             // 0 none, 1 tanh
+  // filled by conv_launch
+  int nchunks, win, bstage, astage;
+  float inv_win;
   int ntm, ntn, nwg;
 };
-int conv_select_cfg(int Cout, int Cin);
+int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation);
+bool conv_cfg_valid(int cfg_id);
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id);
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id);
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
@@ -29,10 +33,14 @@ int snake_launch(const float* x, const float* sa, const float* sb, float* y, int
 int aa_snake_launch(const float* x, const float* sa, const float* sb, const float* fu,
                     const float* fd, float* y, int B, int C, int T, hipStream_t st);
 int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t st);
-int ctb_to_btc_add_launch(const float* y, const float* skip, float* out, int B, int C, int T,
-                          hipStream_t st);
+int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, const float* sb,
+                          float* out, int B, int C, int T, hipStream_t st);
 int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st);
 
+bool lstm_fast_ok(int H);
+void lstm_pack_hh2(const float* w, float* out, int H);
+int lstm_step_frag_launch(const float* gx, const float* whh_p2, const float* hin, float* hout,
+                          float* y, float* cst, int H, int B, int T, int t, hipStream_t st);
 void lstm_pack_hh(const float* w, float* out, int H);
 int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
                      int T, int t, hipStream_t st);

@@ -5,36 +5,46 @@
 // (:115-141), BigCodecEncoder (vq/codec_encoder.py:35-57) and BigCodecDecoder
 // (vq/codec_decoder.py:59-81).  The weight-norm fold w = g*v/||v|| happens once on the host.
 //
-// GEMM view of one conv:  y[b,co,n] = bias[co] + sum_{ci,k} W[co,ci,k] * act(x[b,ci, n*s + k*d - pl])
+// GEMM view of one conv:  y[b,co,n] = bias[co] + sum_{ci,k} W[co,ci,k] * x[b,ci, n*s + k*d - pl]
 //   M = Cout, N = output positions of one clip, K = Cin*taps.
-// act() is the optional fused SnakeBeta prologue (the Activation1d that precedes every conv in the
-// reference), applied while the input tile is staged into LDS.  Epilogue: + bias, optional residual
-// add (ResidualUnit's `x + block(x)`), optional tanh (decoder tail, codec_decoder.py:78-80).
+// Epilogue (fused): + bias, + residual (ResidualUnit's `x + block(x)`), then either tanh (decoder
+// tail) or the SnakeBeta of the NEXT Activation1d (per output channel) — written alone, or beside
+// the raw value when the raw value is still needed as a residual (dual output).  Moving every Snake
+// into the producing conv's epilogue computes it exactly once per element and keeps the operand
+// staging a pure copy.
 //
 // Matrix core: v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).  One 256-thread
 // workgroup computes a BM x BN output tile of one clip: WM x WN waves, each MT x NT 16x16 tiles.
-// K is walked in chunks of BKC input channels; inside a chunk the k index is tap-major
-// (k = tap*BKC + ci_local) so one MFMA k-step (4 values) covers 4 channels of one tap.
-//   LDS A tile : packed weights, [kstep][wave_m][lane] float4 (one ds_read_b128 per lane per k-step)
-//   LDS B tile : snake(x) rows, [ci_local][win] with the stride/dilation halo
-// ConvTranspose1d is run as `stride` polyphase 2-tap convolutions whose outputs are written with
-// output stride `s` (see bc_convT1d_fwd in abi.cpp).
+// K is walked in chunks of BKC input channels; inside a chunk k is tap-major (k = tap*BKC + ci) so
+// one MFMA k-step (4 values) covers 4 channels of one tap.  Both operand tiles of a chunk are
+// copied HBM/L2 -> LDS by LDS-DMA into one of two stages while the other stage feeds the MFMAs
+// (one barrier per chunk):
+//   A (weights): packed [kstep][wave_m][lane] float4, global_load_lds_dwordx4 (1 KiB pieces)
+//   B (input)  : [ci][pitch] rows incl. the stride/dilation halo, buffer_load_dword ... lds with
+//                out-of-range lanes redirected past the buffer end so the hardware returns 0
+//                (zero padding for free).  pitch is chosen so the two 16-lane row groups of a
+//                ds_read_b32 half-wave hit disjoint banks.
+// ConvTranspose1d runs as `stride` polyphase convolutions whose outputs are written with output
+// stride `s` (bc_convT1d_fwd in abi.hip).
 #include "bc_common.h"
 #include "bc_internal.h"
 
 namespace bc {
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+__device__ __forceinline__ lds_ptr_t to_lds(const float* p) {
+  return (lds_ptr_t)(p);
+}
 
-template <int MT, int WM, int NT, int WN, int BKC, bool SNAKE>
+template <int MT, int WM, int NT, int WN, int BKC>
 __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int nks = BKC * a.K / 4;
-  floatx4* As = reinterpret_cast<floatx4*>(smem);           // [nks][WM][64]
-  float* xs = smem + nks * WM * 64 * 4;                      // [BKC][win]
+  const int stage_floats = a.astage + a.bstage;
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int mt_idx = wg % a.ntm;
@@ -46,9 +56,45 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM;
   const int wn = wave / WM;
+
+  // Buffer descriptor of this clip's input; its inputs are made provably wave-uniform
+  // (readfirstlane) so hipcc emits plain buffer loads instead of waterfall loops (guide T20).
+  const unsigned long long xb_u = (unsigned long long)(a.x + (long long)b * a.xbs);
+  const unsigned xb_lo = __builtin_amdgcn_readfirstlane((unsigned)xb_u);
+  const unsigned xb_hi = __builtin_amdgcn_readfirstlane((unsigned)(xb_u >> 32));
+  const int xbytes = __builtin_amdgcn_readfirstlane(a.Cin * a.Tin * 4);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long long)xb_hi << 32) | xb_lo), 0, xbytes, 0x00020000);
+  const int in0 = n0 * a.s - a.pl;
+  const long long mg0 = (long long)mt_idx * WM;
+  const int a_pieces = nks * WM;                 // 1 KiB each
+  const int b_pieces = a.bstage >> 6;            // 64 floats each
+
+  // Issue every LDS-DMA of chunk c into stage st.
+  auto issue = [&](int st, int c) {
+    float* As = smem + st * stage_floats;
+    float* Bs = As + a.astage;
+    const floatx4* wsrc = reinterpret_cast<const floatx4*>(a.w) + (mg0 * a.nchunks + c) * (long long)(nks * 64);
+    for (int q = wave; q < a_pieces; q += 4) {
+      const int ks = q / WM, wm_ = q - ks * WM;
+      const floatx4* src = wsrc + (long long)wm_ * a.nchunks * (nks * 64) + ks * 64 + lane;
+      __builtin_amdgcn_global_load_lds((const void*)src, to_lds(As + q * 256), 16, 0, 0);
+    }
+    const int c0 = c * BKC;
+    for (int p = wave; p < b_pieces; p += 4) {
+      const int f = p * 64 + lane;
+      int row = (int)(((float)f + 0.5f) * a.inv_win);
+      const int col = f - row * a.win;
+      const int ci = c0 + row;
+      const int ti = in0 + col;
+      const bool ok = row < BKC && ci < a.Cin && ti >= 0 && ti < a.Tin;
+      const unsigned voff = ok ? (unsigned)((ci * a.Tin + ti) * 4) : 0xfffffff0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(Bs + p * 64), 4, voff, 0, 0, 0);
+    }
+  };
 
   floatx4 acc[MT][NT];
 #pragma unroll
@@ -56,60 +102,39 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const float* xb = a.x + (long long)b * a.xbs;
-  const int in0 = n0 * a.s - a.pl;
-  const int xs_elems = BKC * a.win;
-  const int a_vecs = nks * WM * 64;
-  const long long mg0 = (long long)mt_idx * WM;
   const int lane_off = ((lane & 15) + wn * NT * 16) * a.s;
   const int krow = lane >> 4;
 
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int c = 0; c < a.nchunks; ++c) {
-    const int c0 = c * BKC;
-    // ---- stage B: snake(x) rows with halo -------------------------------------------------
-    for (int e = tid; e < xs_elems; e += 256) {
-      const int row = e / a.win;
-      const int col = e - row * a.win;
-      const int ci = c0 + row;
-      const int ti = in0 + col;
-      float v = 0.f;
-      if (ci < a.Cin && ti >= 0 && ti < a.Tin) {
-        v = xb[(long long)ci * a.Tin + ti];
-        if constexpr (SNAKE) v = snake(v, a.sa[ci], a.sb[ci]);
-      }
-      xs[e] = v;
-    }
-    // ---- stage A: packed weights for this chunk -------------------------------------------
-    for (int e = tid; e < a_vecs; e += 256) {
-      const int wm_ = e / (nks * 64);
-      const int r = e - wm_ * nks * 64;  // ks*64 + lane
-      const floatx4* src = reinterpret_cast<const floatx4*>(a.w) +
-                           ((mg0 + wm_) * a.nchunks + c) * (long long)(nks * 64) + r;
-      const int ks = r >> 6;
-      As[(ks * WM + wm_) * 64 + (r & 63)] = *src;
-    }
-    __syncthreads();
-    // ---- MFMA over the chunk --------------------------------------------------------------
+    const int st = c & 1;
+    if (c + 1 < a.nchunks) issue(st ^ 1, c + 1);
+    const floatx4* As = reinterpret_cast<const floatx4*>(smem + st * stage_floats);
+    const float* Bs = smem + st * stage_floats + a.astage;
     for (int ks = 0; ks < nks; ++ks) {
       const int kidx = ks * 4;
       const int tap = kidx / BKC;
       const int cb = kidx - tap * BKC;
       const floatx4 av = As[(ks * WM + wm) * 64 + lane];
-      const float* xr = xs + (cb + krow) * a.win + tap * a.d + lane_off;
+      const float* xrow = Bs + (cb + krow) * a.win + tap * a.d + lane_off;
       float bv[NT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bv[j] = xr[j * 16 * a.s];
+      for (int j = 0; j < NT; ++j) bv[j] = xrow[j * 16 * a.s];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ---- epilogue: C/D map of 16x16x4: col = lane&15 (n), row = (lane>>4)*4 + r (m) ----------
   float* yb = a.y + (long long)b * a.ybs;
+  float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -118,6 +143,8 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
       const int co = m0 + wm * MT * 16 + i * 16 + (lane >> 4) * 4 + r;
       if (co >= a.Cout) continue;
       const float bias = a.bias ? a.bias[co] : 0.f;
+      const float sa = a.osa ? a.osa[co] : 0.f;
+      const float sb = a.osa ? a.osb[co] : 0.f;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = n0 + wn * NT * 16 + j * 16 + (lane & 15);
@@ -126,7 +153,17 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
         float v = acc[i][j][r] + bias;
         if (rb) v = rb[yi] + v;
         if (a.epi == 1) v = tanhf(v);
-        yb[yi] = v;
+        if (a.osa) {
+          const float sv = snake(v, sa, sb);
+          if (y2b) {
+            yb[yi] = v;
+            y2b[yi] = sv;
+          } else {
+            yb[yi] = sv;
+          }
+        } else {
+          yb[yi] = v;
+        }
       }
     }
   }
@@ -134,41 +171,92 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // Host side: tile-config table, weight packing, launch.
+// cfg id = tile * 4 + bkc_index; tile by Cout, BKC (input channels per K chunk) by shape.
 // ------------------------------------------------------------------------------------------------
-struct TileCfg {
-  int MT, WM, NT, WN, BKC;
+struct Tile {
+  int MT, WM, NT, WN;
 };
-static const TileCfg kCfgs[] = {
-    {4, 2, 4, 2, 8},  // 0: BM=128 BN=128
-    {4, 1, 4, 4, 8},  // 1: BM=64  BN=256
-    {3, 1, 4, 4, 8},  // 2: BM=48  BN=256
-    {2, 1, 4, 4, 8},  // 3: BM=32  BN=256
-    {1, 1, 4, 4, 8},  // 4: BM=16  BN=256
-    {4, 2, 4, 2, 4},  // 5..9: same tiles, BKC=4 (Cin < 8, e.g. the first conv Cin=1)
-    {4, 1, 4, 4, 4},
-    {3, 1, 4, 4, 4},
-    {2, 1, 4, 4, 4},
-    {1, 1, 4, 4, 4},
+static const Tile kTiles[] = {
+    {4, 2, 4, 2},  // 0: BM=128 BN=128   (Cout >= 128)
+    {4, 1, 4, 4},  // 1: BM=64  BN=256
+    {3, 1, 4, 4},  // 2: BM=48  BN=256
+    {2, 1, 4, 4},  // 3: BM=32  BN=256
+    {1, 1, 4, 4},  // 4: BM=16  BN=256
 };
-
-int conv_select_cfg(int Cout, int Cin) {
-  int base;
-  if (Cout >= 128) base = 0;
-  else if (Cout > 48) base = 1;
-  else if (Cout > 32) base = 2;
-  else if (Cout > 16) base = 3;
-  else base = 4;
-  return Cin < 8 ? base + 5 : base;
+static const int kBKC[] = {32, 16, 8, 4};
+// Bytes per LDS stage (two stages per workgroup).  BC_STAGE_BUDGET_KB overrides it for tuning
+// experiments; weight packing and launch read the same value, so they always agree in-process.
+static int stage_budget() {
+  static int v = [] {
+    const char* e = getenv("BC_STAGE_BUDGET_KB");
+    const int kb = e ? atoi(e) : 40;
+    return (kb >= 8 && kb <= 78 ? kb : 40) * 1024;
+  }();
+  return v;
 }
 
-static inline int cfg_BM(const TileCfg& t) { return 16 * t.MT * t.WM; }
-static inline int cfg_BN(const TileCfg& t) { return 16 * t.NT * t.WN; }
+static inline int tile_BM(const Tile& t) { return 16 * t.MT * t.WM; }
+static inline int tile_BN(const Tile& t) { return 16 * t.NT * t.WN; }
+
+// Input-tile row pitch: covers (BN-1)*s + (K-1)*d + 1 columns, padded so the two 16-lane row
+// groups of a ds_read_b32 half-wave land on disjoint banks (bank = dword index mod 32).
+static int choose_pitch(int need, int s) {
+  int best = need, best_conf = 1 << 30;
+  for (int pad = 0; pad < 32; ++pad) {
+    const int w = need + pad;
+    int cnt[32] = {0};
+    for (int l = 0; l < 32; ++l) cnt[((l >> 4) * w + (l & 15) * s) & 31]++;
+    int conf = 0;
+    for (int k = 0; k < 32; ++k) conf = conf > cnt[k] ? conf : cnt[k];
+    if (conf < best_conf) {
+      best_conf = conf;
+      best = w;
+    }
+    if (conf == 1) break;
+  }
+  return best;
+}
+
+static inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+struct Geometry {
+  int pitch, bstage, astage, nks;
+};
+static Geometry geometry(const Tile& t, int bkc, int K, int s, int d) {
+  Geometry g;
+  g.pitch = choose_pitch((tile_BN(t) - 1) * s + (K - 1) * d + 1, s);
+  g.bstage = round_up(bkc * g.pitch, 64);
+  g.nks = bkc * K / 4;
+  g.astage = g.nks * t.WM * 256;
+  return g;
+}
+
+int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation) {
+  int tile;
+  if (Cout >= 128) tile = 0;
+  else if (Cout > 48) tile = 1;
+  else if (Cout > 32) tile = 2;
+  else if (Cout > 16) tile = 3;
+  else tile = 4;
+  const Tile& t = kTiles[tile];
+  for (int bi = 0; bi < 4; ++bi) {
+    const int bkc = kBKC[bi];
+    if (bkc > 4 && bkc > round_up(Cin, 4)) continue;  // do not pad the channel chunk past Cin
+    const Geometry g = geometry(t, bkc, K, stride, dilation);
+    if (g.nks > 40) continue;
+    if ((g.astage + g.bstage) * 4 <= stage_budget()) return tile * 4 + bi;
+  }
+  return tile * 4 + 3;  // BKC = 4 always fits the shapes the codec builds
+}
+
+bool conv_cfg_valid(int cfg_id) { return cfg_id >= 0 && cfg_id < 20; }
 
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id) {
-  const TileCfg& t = kCfgs[cfg_id];
-  const int ntm = (Cout + cfg_BM(t) - 1) / cfg_BM(t);
-  const int nchunks = (Cin + t.BKC - 1) / t.BKC;
-  const int nks = t.BKC * K / 4;
+  const Tile& t = kTiles[cfg_id / 4];
+  const int bkc = kBKC[cfg_id % 4];
+  const int ntm = (Cout + tile_BM(t) - 1) / tile_BM(t);
+  const int nchunks = (Cin + bkc - 1) / bkc;
+  const int nks = bkc * K / 4;
   return (long long)ntm * t.WM * nchunks * nks * 64 * 4;
 }
 
@@ -176,11 +264,12 @@ long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id) {
 // Layout: [mgroup][chunk][kstep][lane][4]; mgroup = 16*MT output rows; element i of the float4 is
 // m-tile i (zero for i >= MT); lane -> (row = lane&15, k = 4*kstep + (lane>>4)), k tap-major.
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id) {
-  const TileCfg& t = kCfgs[cfg_id];
-  const int ntm = (Cout + cfg_BM(t) - 1) / cfg_BM(t);
+  const Tile& t = kTiles[cfg_id / 4];
+  const int bkc = kBKC[cfg_id % 4];
+  const int ntm = (Cout + tile_BM(t) - 1) / tile_BM(t);
   const int nmg = ntm * t.WM;
-  const int nchunks = (Cin + t.BKC - 1) / t.BKC;
-  const int nks = t.BKC * K / 4;
+  const int nchunks = (Cin + bkc - 1) / bkc;
+  const int nks = bkc * K / 4;
   long long o = 0;
   for (int mg = 0; mg < nmg; ++mg)
     for (int c = 0; c < nchunks; ++c)
@@ -191,70 +280,54 @@ void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int 
             if (i < t.MT) {
               const int row = mg * 16 * t.MT + i * 16 + (lane & 15);
               const int kidx = ks * 4 + (lane >> 4);
-              const int tap = kidx / t.BKC;
-              const int ci = c * t.BKC + (kidx % t.BKC);
+              const int tap = kidx / bkc;
+              const int ci = c * bkc + (kidx % bkc);
               if (row < Cout && ci < Cin) v = w[((long long)row * Cin + ci) * K + tap];
             }
             out[o] = v;
           }
 }
 
-// Input-tile row length: covers (BN-1)*s + (K-1)*d + 1 columns, padded so the two 16-lane row
-// groups of a ds_read_b32 half-wave land on disjoint banks (bank = dword index mod 32).
-static int choose_win(int need, int s) {
-  int best = need, best_conf = 1 << 30;
-  for (int pad = 0; pad < 32; ++pad) {
-    const int w = need + pad;
-    int cnt[32] = {0};
-    for (int l = 0; l < 32; ++l) {
-      const int addr = (l >> 4) * w + (l & 15) * s;
-      cnt[addr & 31]++;
-    }
-    int conf = 0;
-    for (int k = 0; k < 32; ++k) conf = conf > cnt[k] ? conf : cnt[k];
-    if (conf < best_conf) { best_conf = conf; best = w; }
-    if (conf == 1) break;
-  }
-  return best;
-}
-
 template <int MT, int WM, int NT, int WN, int BKC>
-static int launch_cfg(ConvArgs& a, int B, hipStream_t st) {
+static int launch_tile(ConvArgs& a, int B, hipStream_t st) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const Tile t{MT, WM, NT, WN};
+  const Geometry g = geometry(t, BKC, a.K, a.s, a.d);
   a.ntm = (a.Cout + BM - 1) / BM;
   a.ntn = (a.Nout + BN - 1) / BN;
   a.nchunks = (a.Cin + BKC - 1) / BKC;
-  a.win = choose_win((BN - 1) * a.s + (a.K - 1) * a.d + 1, a.s);
+  a.win = g.pitch;
+  a.inv_win = 1.0f / (float)g.pitch;
+  a.bstage = g.bstage;
+  a.astage = g.astage;
   const long long nwg = (long long)a.ntm * a.ntn * B;
   if (nwg <= 0) return BC_OK;
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;  // buffer range
   a.nwg = (int)nwg;
-  const int nks = BKC * a.K / 4;
-  const size_t lds = (size_t)nks * WM * 64 * 16 + (size_t)BKC * a.win * 4;
+  const size_t lds = (size_t)2 * (g.astage + g.bstage) * 4;
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  if (a.sa)
-    hipLaunchKernelGGL((conv1d_mfma_kernel<MT, WM, NT, WN, BKC, true>), dim3(a.nwg), dim3(256), lds, st, a);
-  else
-    hipLaunchKernelGGL((conv1d_mfma_kernel<MT, WM, NT, WN, BKC, false>), dim3(a.nwg), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv1d_mfma_kernel<MT, WM, NT, WN, BKC>), dim3(a.nwg), dim3(256), lds, st, a);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
 
+#define BC_TILE_CASES(T, MT, WM, NT, WN)                              \
+  case T * 4 + 0: return launch_tile<MT, WM, NT, WN, 32>(a, B, st);   \
+  case T * 4 + 1: return launch_tile<MT, WM, NT, WN, 16>(a, B, st);   \
+  case T * 4 + 2: return launch_tile<MT, WM, NT, WN, 8>(a, B, st);    \
+  case T * 4 + 3: return launch_tile<MT, WM, NT, WN, 4>(a, B, st);
+
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st) {
-  if (a.K * 8 % 4 != 0) return BC_ERR_ARG;
   switch (cfg_id) {
-    case 0: return launch_cfg<4, 2, 4, 2, 8>(a, B, st);
-    case 1: return launch_cfg<4, 1, 4, 4, 8>(a, B, st);
-    case 2: return launch_cfg<3, 1, 4, 4, 8>(a, B, st);
-    case 3: return launch_cfg<2, 1, 4, 4, 8>(a, B, st);
-    case 4: return launch_cfg<1, 1, 4, 4, 8>(a, B, st);
-    case 5: return launch_cfg<4, 2, 4, 2, 4>(a, B, st);
-    case 6: return launch_cfg<4, 1, 4, 4, 4>(a, B, st);
-    case 7: return launch_cfg<3, 1, 4, 4, 4>(a, B, st);
-    case 8: return launch_cfg<2, 1, 4, 4, 4>(a, B, st);
-    case 9: return launch_cfg<1, 1, 4, 4, 4>(a, B, st);
+    BC_TILE_CASES(0, 4, 2, 4, 2)
+    BC_TILE_CASES(1, 4, 1, 4, 4)
+    BC_TILE_CASES(2, 3, 1, 4, 4)
+    BC_TILE_CASES(3, 2, 1, 4, 4)
+    BC_TILE_CASES(4, 1, 1, 4, 4)
   }
   return BC_ERR_ARG;
 }
+#undef BC_TILE_CASES
 
 }  // namespace bc

@@ -112,9 +112,12 @@ __global__ void __launch_bounds__(256) btc_to_ctb_kernel(const float* __restrict
   }
 }
 
-// out[B][C][T] = y[C][T][B] + skip[B][C][T]   (ResLSTM skip, vq/module.py:163-166)
+// out[B][C][T] = act(y[C][T][B] + skip[B][C][T])   (ResLSTM skip, vq/module.py:163-166; act = the
+// following Activation1d's Snake when sa != nullptr, fused so the LSTM output is written once)
 __global__ void __launch_bounds__(256) ctb_to_btc_add_kernel(const float* __restrict__ yin,
                                                              const float* __restrict__ skip,
+                                                             const float* __restrict__ sa,
+                                                             const float* __restrict__ sb,
                                                              float* __restrict__ out, int B, int C,
                                                              int T) {
   __shared__ float tl[64][33];
@@ -131,7 +134,8 @@ __global__ void __launch_bounds__(256) ctb_to_btc_add_kernel(const float* __rest
     const int b = b0 + bl, t = t0 + tl_;
     if (b < B && t < T) {
       const long long i = ((long long)b * C + c) * T + t;
-      out[i] = tl[bl][tl_] + skip[i];
+      const float v = tl[bl][tl_] + skip[i];
+      out[i] = sa ? snake(v, sa[c], sb[c]) : v;
     }
   }
 }
@@ -186,11 +190,11 @@ int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t
   return BC_OK;
 }
 
-int ctb_to_btc_add_launch(const float* y, const float* skip, float* out, int B, int C, int T,
-                          hipStream_t st) {
+int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, const float* sb,
+                          float* out, int B, int C, int T, hipStream_t st) {
   if ((long long)B * C * T == 0) return BC_OK;
   dim3 grid((T + 31) / 32, C, (B + 63) / 64);
-  hipLaunchKernelGGL(ctb_to_btc_add_kernel, grid, dim3(256), 0, st, y, skip, out, B, C, T);
+  hipLaunchKernelGGL(ctb_to_btc_add_kernel, grid, dim3(256), 0, st, y, skip, sa, sb, out, B, C, T);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

@@ -1,22 +1,19 @@
-"""BigCodec modules with the reference's constructor signatures and state_dict layout, computing on
-the gfx950 HIP kernels of libbigcodec_hip.so.
+"""Activations (vq/activations.py, vq/alias_free_torch/) and the factorized VQ
+(vq/factorized_vector_quantize.py, vq/residual_vq.py) with the reference's constructor signatures
+and state_dict layout, computing on the gfx950 HIP kernels of libbigcodec_hip.so.
 
-Drop-in surface: every class here has the same name, constructor arguments,
-parameter/buffer names and forward signature as its counterpart in the reference's vq/ package,
-so a reference state_dict loads strictly and the callers (lightning_module.py:266-285,
-extract_indices.py:353-363, inference_full.py:557-561) work unchanged.  Forward passes run only
-on device tensors (fp32); there is no CPU / eager fallback — a CPU input raises.
-
-Composite modules run fused kernels: the Snake of every Activation1d is applied inside the input
-staging of the conv that follows it, and ResidualUnit's skip add is the second conv's epilogue.
-Folded weights (weight-norm g*v/||v|| evaluated by torch._weight_norm on the CPU, bit-identical
-to the reference's per-forward recomputation) are packed once per parameter version and cached
-on the device.
+Drop-in surface: every class here, in conv.py and in blocks.py has the same name,
+constructor arguments, parameter/buffer names and forward signature as its counterpart in the
+reference's vq/ package, so a reference state_dict loads strictly and the callers
+(lightning_module.py:266-285, extract_indices.py:353-363, inference_full.py:557-561) work
+unchanged.  Forward passes run only on device tensors (fp32); there is no CPU / eager fallback — a
+CPU input raises.  Host-side parameter preparation (weight-norm folding with torch._weight_norm on
+the CPU, bit-identical to the reference's per-forward recomputation; per-channel Snake
+coefficients) happens once per parameter version and is cached on the device.
 """
 from __future__ import annotations
 
 import math
-from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -27,9 +24,7 @@ from . import _lib as L
 
 __all__ = [
     "SnakeBeta", "Snake", "Activation1d", "UpSample1d", "DownSample1d", "LowPassFilter1d",
-    "kaiser_sinc_filter1d", "WNConv1d", "WNConvTranspose1d", "CausalConv1d", "CausalConvTranspose1d",
-    "Conv1dWN", "ConvTranspose1dWN", "ResidualUnit", "EncoderBlock", "DecoderBlock", "LSTM", "ResLSTM",
-    "FactorizedVectorQuantize", "ResidualVQ",
+    "kaiser_sinc_filter1d", "LinearWN", "FactorizedVectorQuantize", "ResidualVQ",
 ]
 
 
@@ -65,6 +60,19 @@ class _DeviceCache:
 
 def _cpu(t: torch.Tensor) -> torch.Tensor:
     return t.detach().to("cpu", torch.float32)
+
+
+_ZEROS = {}
+
+
+def _zeros(n: int, device) -> torch.Tensor:
+    """Cached all-zero fp32 device vector (the eval-mode VQ losses): uploaded once, no fill kernel
+    per call.  Callers must not write into it."""
+    key = (n, str(device))
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros(n).to(device)
+    return z
 
 
 # ------------------------------------------------------------------------------------------------
@@ -259,412 +267,6 @@ class Activation1d(nn.Module):
         return y
 
 
-def run_activation_then(act: Activation1d, x: torch.Tensor):
-    """Return (input for the next conv, snake coefficients to fuse or None)."""
-    co = act.snake_coeffs(x.device)
-    if co is not None:
-        return x, co
-    return act(x), None
-
-
-# ------------------------------------------------------------------------------------------------
-# convolutions  (vq/module.py:11-72)
-# ------------------------------------------------------------------------------------------------
-class Conv1dWN(nn.Module):
-    """weight_norm(nn.Conv1d(...)) with the same parameter names (bias, weight_g, weight_v) and the
-    same constructor signature as nn.Conv1d (groups=1, padding_mode='zeros')."""
-
-    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
-                 groups=1, bias=True, padding_mode="zeros", device=None, dtype=None):
-        super().__init__()
-        if groups != 1 or padding_mode != "zeros":
-            raise NotImplementedError("only groups=1, padding_mode='zeros' (all the reference uses)")
-        if isinstance(padding, str):
-            raise NotImplementedError("string padding is not used by the reference")
-        self.in_channels, self.out_channels = in_channels, out_channels
-        self.kernel_size = int(kernel_size[0] if isinstance(kernel_size, (tuple, list)) else kernel_size)
-        self.stride = int(stride[0] if isinstance(stride, (tuple, list)) else stride)
-        self.padding = int(padding[0] if isinstance(padding, (tuple, list)) else padding)
-        self.dilation = int(dilation[0] if isinstance(dilation, (tuple, list)) else dilation)
-        self.causal_pad: Optional[int] = None  # set by CausalConv1d
-        ref = nn.Conv1d(in_channels, out_channels, self.kernel_size, bias=bias)  # default init
-        if bias:
-            self.bias = Parameter(ref.bias.detach().clone().zero_())
-        else:
-            self.register_parameter("bias", None)
-        v = ref.weight.detach().clone()
-        self.weight_g = Parameter(torch.linalg.vector_norm(v.reshape(v.shape[0], -1), dim=1).reshape(-1, 1, 1))
-        self.weight_v = Parameter(v)
-        self._cache = _DeviceCache()
-
-    def folded_weight(self) -> torch.Tensor:
-        if "weight" in self._parameters:
-            return _cpu(self._parameters["weight"])
-        return torch._weight_norm(_cpu(self.weight_v), _cpu(self.weight_g), 0)
-
-    def remove_weight_norm(self):
-        w = self.folded_weight()
-        del self._parameters["weight_g"]
-        del self._parameters["weight_v"]
-        self.weight = Parameter(w.to(self.bias.device if self.bias is not None else "cpu"))
-
-    def _params(self):
-        if "weight" in self._parameters:
-            return (self._parameters["weight"], self.bias)
-        return (self.weight_g, self.weight_v, self.bias)
-
-    def prepared(self, device):
-        def build():
-            w = self.folded_weight().contiguous()
-            Cout, Cin, K = w.shape
-            cfg = L.load().bc_conv1d_select_cfg(Cout, Cin)
-            n = L.load().bc_conv1d_packed_floats(Cout, Cin, K, cfg)
-            packed = np.empty(n, dtype=np.float32)
-            wn = w.numpy()
-            L.call("bc_conv1d_pack", wn.ctypes.data, packed.ctypes.data, Cout, Cin, K, cfg)
-            bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
-            return torch.from_numpy(packed).to(device), bias, cfg
-        return self._cache.get(_pkey(*self._params()) + (str(device),), build)
-
-    def out_len(self, T: int) -> int:
-        pl = self.pad_left()
-        pr = 0 if self.causal_pad is not None else self.padding
-        return (T + pl + pr - self.dilation * (self.kernel_size - 1) - 1) // self.stride + 1
-
-    def pad_left(self) -> int:
-        return self.causal_pad if self.causal_pad is not None else self.padding
-
-    def run(self, x, snake=None, residual=None, epilogue: int = 0):
-        x = _as_input(x)
-        B, Cin, T = x.shape
-        if Cin != self.in_channels:
-            raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
-        wp, bias, cfg = self.prepared(x.device)
-        Tout = self.out_len(T)
-        if Tout <= 0:
-            raise ValueError(f"input length {T} too short for this convolution")
-        y = torch.empty((B, self.out_channels, Tout), device=x.device, dtype=torch.float32)
-        if residual is not None:
-            residual = _as_input(residual)
-            if residual.shape != y.shape:
-                raise ValueError(f"residual shape {tuple(residual.shape)} != output {tuple(y.shape)}")
-        sa, sb = snake if snake is not None else (None, None)
-        tm = L.active_timer()
-        ev = tm.begin() if tm is not None else None
-        L.call("bc_conv1d_fwd", x.data_ptr(), wp.data_ptr(), L.ptr(bias), L.ptr(sa), L.ptr(sb),
-               L.ptr(residual), y.data_ptr(), B, Cin, T, self.out_channels, Tout, self.kernel_size,
-               self.stride, self.dilation, self.pad_left(), epilogue, cfg, L.stream_of(x))
-        if tm is not None:
-            flops = 2.0 * B * self.out_channels * Cin * self.kernel_size * Tout
-            nbytes = 4.0 * (x.numel() + y.numel() * (2 if residual is not None else 1))
-            tm.end(ev, L.conv_kernel_name(cfg, snake is not None), flops, nbytes)
-        return y
-
-    def forward(self, x):
-        return self.run(x)
-
-
-class CausalConv1d(nn.Module):
-    """vq/module.py:11-48: left zero-pad (k - s) * d, then conv; parameters under `.conv`."""
-
-    def __init__(self, in_channels, out_channels, kernel_size, padding=0, stride=1, dilation=1, groups=1,
-                 bias=True, padding_mode="zeros", device=None, dtype=None):
-        super().__init__()
-        self.conv = Conv1dWN(in_channels, out_channels, kernel_size, stride=stride, padding=0,
-                             dilation=dilation, groups=groups, bias=bias)
-        self.padding_mode = "constant" if padding_mode == "zeros" else padding_mode
-        self.padding = (kernel_size - stride) * dilation
-        self.conv.causal_pad = self.padding
-
-    def run(self, x, snake=None, residual=None, epilogue: int = 0):
-        return self.conv.run(x, snake, residual, epilogue)
-
-    def forward(self, x):
-        return self.conv.run(x)
-
-    @property
-    def in_channels(self):
-        return self.conv.in_channels
-
-    @property
-    def out_channels(self):
-        return self.conv.out_channels
-
-
-def WNConv1d(*args, causal=False, **kwargs):
-    """vq/module.py:59-65."""
-    if causal:
-        return CausalConv1d(*args, **kwargs)
-    return Conv1dWN(*args, **kwargs)
-
-
-class ConvTranspose1dWN(nn.Module):
-    """weight_norm(nn.ConvTranspose1d(...)): weight_v (Cin, Cout, K), weight_g (Cin, 1, 1) — the
-    norm runs over dim 0 = INPUT channels — and bias (Cout)."""
-
-    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, output_padding=0,
-                 groups=1, bias=True, dilation=1, padding_mode="zeros", device=None, dtype=None):
-        super().__init__()
-        if groups != 1 or dilation != 1:
-            raise NotImplementedError("only groups=1, dilation=1 (all the reference uses)")
-        self.in_channels, self.out_channels = in_channels, out_channels
-        self.kernel_size = int(kernel_size)
-        self.stride = int(stride)
-        self.padding = int(padding)
-        self.output_padding = int(output_padding)
-        self.causal_crop = 0  # set by CausalConvTranspose1d
-        ref = nn.ConvTranspose1d(in_channels, out_channels, self.kernel_size, stride, bias=bias)
-        if bias:
-            self.bias = Parameter(ref.bias.detach().clone())
-        else:
-            self.register_parameter("bias", None)
-        v = ref.weight.detach().clone()
-        self.weight_g = Parameter(torch.linalg.vector_norm(v.reshape(v.shape[0], -1), dim=1).reshape(-1, 1, 1))
-        self.weight_v = Parameter(v)
-        self._cache = _DeviceCache()
-
-    def folded_weight(self) -> torch.Tensor:
-        if "weight" in self._parameters:
-            return _cpu(self._parameters["weight"])
-        return torch._weight_norm(_cpu(self.weight_v), _cpu(self.weight_g), 0)
-
-    def remove_weight_norm(self):
-        w = self.folded_weight()
-        del self._parameters["weight_g"]
-        del self._parameters["weight_v"]
-        self.weight = Parameter(w.to(self.bias.device if self.bias is not None else "cpu"))
-
-    def _params(self):
-        if "weight" in self._parameters:
-            return (self._parameters["weight"], self.bias)
-        return (self.weight_g, self.weight_v, self.bias)
-
-    def prepared(self, device):
-        def build():
-            w = self.folded_weight()  # (Cin, Cout, K)
-            Cin, Cout, K = w.shape
-            s = self.stride
-            lib = L.load()
-            Kp = lib.bc_convT1d_phase_taps(K, s)
-            cfg = lib.bc_conv1d_select_cfg(Cout, Cin)
-            n = lib.bc_conv1d_packed_floats(Cout, Cin, Kp, cfg)
-            wt = w.permute(1, 0, 2).contiguous()  # (Cout, Cin, K)
-            phases = []
-            for r in range(s):
-                wr = torch.zeros(Cout, Cin, Kp, dtype=torch.float32)
-                for jp in range(Kp):
-                    k = r + s * (Kp - 1 - jp)
-                    if k < K:
-                        wr[:, :, jp] = wt[:, :, k]
-                packed = np.empty(n, dtype=np.float32)
-                wrn = wr.contiguous().numpy()
-                L.call("bc_conv1d_pack", wrn.ctypes.data, packed.ctypes.data, Cout, Cin, Kp, cfg)
-                phases.append(torch.from_numpy(packed).to(device))
-            bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
-            return phases, L.ptr_array([p.data_ptr() for p in phases]), bias, cfg
-        return self._cache.get(_pkey(*self._params()) + (str(device),), build)
-
-    def out_len(self, T: int) -> int:
-        full = (T - 1) * self.stride - 2 * self.padding + self.kernel_size + self.output_padding
-        return full - self.causal_crop
-
-    def run(self, x, snake=None):
-        x = _as_input(x)
-        B, Cin, T = x.shape
-        if Cin != self.in_channels:
-            raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
-        _, parr, bias, cfg = self.prepared(x.device)
-        Tout = self.out_len(T)
-        y = torch.empty((B, self.out_channels, Tout), device=x.device, dtype=torch.float32)
-        sa, sb = snake if snake is not None else (None, None)
-        L.call("bc_convT1d_fwd", x.data_ptr(), parr, L.ptr(bias), L.ptr(sa), L.ptr(sb), y.data_ptr(), B,
-               Cin, T, self.out_channels, Tout, self.kernel_size, self.stride, self.padding, cfg,
-               L.stream_of(x))
-        return y
-
-    def forward(self, x):
-        return self.run(x)
-
-
-class CausalConvTranspose1d(nn.Module):
-    """vq/module.py:50-57: transposed conv without padding, last `stride` samples cropped."""
-
-    def __init__(self, in_channels, out_channels, kernel_size, stride=1, bias=True, device=None, dtype=None):
-        super().__init__()
-        self.conv = ConvTranspose1dWN(in_channels, out_channels, kernel_size, stride, bias=bias)
-        self.stride = stride
-        self.conv.causal_crop = stride
-
-    def run(self, x, snake=None):
-        return self.conv.run(x, snake)
-
-    def forward(self, x):
-        return self.conv.run(x)
-
-
-def WNConvTranspose1d(*args, causal=False, **kwargs):
-    """vq/module.py:67-72."""
-    if causal:
-        return CausalConvTranspose1d(*args, **kwargs)
-    return ConvTranspose1dWN(*args, **kwargs)
-
-
-def _conv_of(m) -> Conv1dWN:
-    return m.conv if isinstance(m, CausalConv1d) else m
-
-
-# ------------------------------------------------------------------------------------------------
-# blocks  (vq/module.py:74-167)
-# ------------------------------------------------------------------------------------------------
-class ResidualUnit(nn.Module):
-    """vq/module.py:74-89: x + conv1(snake(conv7_d(snake(x)))) as two fused launches:
-    conv7 with the first Snake in its prologue, conv1 with the second Snake in its prologue and
-    the skip add in its epilogue."""
-
-    def __init__(self, dim: int = 16, dilation: int = 1, causal: bool = False, antialias: bool = False):
-        super().__init__()
-        pad = 0 if causal else ((7 - 1) * dilation) // 2
-        self.block = nn.Sequential(
-            Activation1d(activation=SnakeBeta(dim, alpha_logscale=True), antialias=antialias),
-            WNConv1d(dim, dim, kernel_size=7, dilation=dilation, padding=pad, causal=causal),
-            Activation1d(activation=SnakeBeta(dim, alpha_logscale=True), antialias=antialias),
-            WNConv1d(dim, dim, kernel_size=1),
-        )
-
-    def forward(self, x):
-        x = _as_input(x)
-        h, co = run_activation_then(self.block[0], x)
-        h = self.block[1].run(h, snake=co)
-        h, co = run_activation_then(self.block[2], h)
-        return self.block[3].run(h, snake=co, residual=x)
-
-
-class EncoderBlock(nn.Module):
-    """vq/module.py:91-113: 3 ResidualUnits -> Snake -> strided conv (k=2s) C/2 -> C."""
-
-    def __init__(self, dim: int = 16, stride: int = 1, dilations=(1, 3, 9), causal: bool = False,
-                 antialias: bool = False):
-        super().__init__()
-        runits = [ResidualUnit(dim // 2, dilation=d, causal=causal, antialias=antialias) for d in dilations]
-        pad = 0 if causal else (stride // 2 + stride % 2 if stride != 1 else 0)
-        self.block = nn.Sequential(
-            *runits,
-            Activation1d(activation=SnakeBeta(dim // 2, alpha_logscale=True), antialias=antialias),
-            WNConv1d(dim // 2, dim, kernel_size=2 * stride if stride != 1 else 1, stride=stride,
-                     padding=pad, causal=causal),
-        )
-
-    def forward(self, x):
-        n = len(self.block)
-        for i in range(n - 2):
-            x = self.block[i](x)
-        h, co = run_activation_then(self.block[n - 2], x)
-        return self.block[n - 1].run(h, snake=co)
-
-
-class DecoderBlock(nn.Module):
-    """vq/module.py:115-141: Snake -> transposed conv (k=2s) -> 3 ResidualUnits."""
-
-    def __init__(self, input_dim: int = 16, output_dim: int = 8, stride: int = 1, dilations=(1, 3, 9),
-                 causal: bool = False, antialias: bool = False):
-        super().__init__()
-        if causal:
-            tconv_kwargs = {}
-        else:
-            tconv_kwargs = {"padding": stride // 2 + stride % 2 if stride != 1 else 0,
-                            "output_padding": stride % 2 if stride != 1 else 0}
-        self.block = nn.Sequential(
-            Activation1d(activation=SnakeBeta(input_dim, alpha_logscale=True), antialias=antialias),
-            WNConvTranspose1d(input_dim, output_dim, kernel_size=2 * stride if stride != 1 else 1,
-                              stride=stride, causal=causal, **tconv_kwargs),
-        )
-        self.block.extend([ResidualUnit(output_dim, dilation=d, causal=causal, antialias=antialias)
-                           for d in dilations])
-
-    def forward(self, x):
-        x = _as_input(x)
-        h, co = run_activation_then(self.block[0], x)
-        x = self.block[1].run(h, snake=co)
-        for i in range(2, len(self.block)):
-            x = self.block[i](x)
-        return x
-
-
-class LSTM(nn.Module):
-    """Parameter container with torch.nn.LSTM's names (weight_ih_l{k}, weight_hh_l{k}, bias_ih_l{k},
-    bias_hh_l{k}; batch_first) so reference checkpoints load; the recurrence runs in
-    bc_reslstm_fwd."""
-
-    def __init__(self, input_size, hidden_size, num_layers=1, bias=True, batch_first=True,
-                 dropout=0.0, bidirectional=False):
-        super().__init__()
-        if bidirectional:
-            raise NotImplementedError("bidirectional ResLSTM is not used by any shipped config")
-        if not bias or not batch_first or dropout:
-            raise NotImplementedError("only bias=True, batch_first=True, dropout=0")
-        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
-        self.batch_first, self.bidirectional = batch_first, bidirectional
-        ref = nn.LSTM(input_size, hidden_size, num_layers, batch_first=True)  # torch's default init
-        for name, p in ref.named_parameters():
-            setattr(self, name, Parameter(p.detach().clone()))
-        self._cache = _DeviceCache()
-
-    def _plist(self):
-        out = []
-        for l in range(self.num_layers):
-            out += [getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"),
-                    getattr(self, f"bias_ih_l{l}"), getattr(self, f"bias_hh_l{l}")]
-        return out
-
-    def prepared(self, device):
-        def build():
-            lib = L.load()
-            H = self.hidden_size
-            if self.input_size != H:
-                raise NotImplementedError("ResLSTM requires input_size == hidden_size")
-            cfg = lib.bc_conv1d_select_cfg(4 * H, H)
-            wih, whh, bias = [], [], []
-            for l in range(self.num_layers):
-                w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
-                n = lib.bc_conv1d_packed_floats(4 * H, H, 1, cfg)
-                packed = np.empty(n, dtype=np.float32)
-                L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
-                wih.append(torch.from_numpy(packed).to(device))
-                w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
-                packed = np.empty(lib.bc_lstm_hh_packed_floats(H), dtype=np.float32)
-                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H)
-                whh.append(torch.from_numpy(packed).to(device))
-                b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
-                bias.append(b.contiguous().to(device))
-            arrs = (L.ptr_array([t.data_ptr() for t in wih]), L.ptr_array([t.data_ptr() for t in bias]),
-                    L.ptr_array([t.data_ptr() for t in whh]))
-            return (wih, whh, bias), arrs
-        return self._cache.get(_pkey(*self._plist()) + (str(device),), build)
-
-
-class ResLSTM(nn.Module):
-    """vq/module.py:143-167: y = LSTM(x^T)^T + x for x (B, F, T)."""
-
-    def __init__(self, dimension: int, num_layers: int = 2, bidirectional: bool = False, skip: bool = True):
-        super().__init__()
-        if not skip:
-            raise NotImplementedError("ResLSTM(skip=False) is not used by the reference models")
-        self.skip = skip
-        self.lstm = LSTM(dimension, dimension if not bidirectional else dimension // 2, num_layers,
-                         batch_first=True, bidirectional=bidirectional)
-
-    def forward(self, x):
-        x = _as_input(x)
-        B, H, T = x.shape
-        _, (pwih, pbias, pwhh) = self.lstm.prepared(x.device)
-        lib = L.load()
-        ws = torch.empty(int(lib.bc_lstm_workspace_floats(B, H, T)), device=x.device, dtype=torch.float32)
-        y = torch.empty_like(x)
-        L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias,
-               pwhh, ws.data_ptr(), L.stream_of(x))
-        return y
-
-
 # ------------------------------------------------------------------------------------------------
 # quantizer  (vq/factorized_vector_quantize.py, vq/residual_vq.py)
 # ------------------------------------------------------------------------------------------------
@@ -761,7 +363,7 @@ class FactorizedVectorQuantize(nn.Module):
         idx = torch.empty((B, T), device=z.device, dtype=torch.int64)
         post = torch.empty_like(z)
         self.quantize_into(z, idx, post)
-        commit_loss = torch.zeros(B, device=z.device)
+        commit_loss = _zeros(B, z.device)  # eval: torch.zeros(B) (factorized_vector_quantize.py:66)
         return post, idx, commit_loss
 
     def vq2emb(self, vq, proj=True):
@@ -820,7 +422,7 @@ class ResidualVQ(nn.Module):
         if self.training and torch.is_grad_enabled():
             raise NotImplementedError("training-mode VQ is out of scope of the HIP inference path; call .eval()")
         quantized_out, all_indices = self.quantize(x)
-        all_losses = torch.zeros(len(self.layers), device=quantized_out.device)
+        all_losses = _zeros(len(self.layers), quantized_out.device)  # stack of zeros(B).mean()
         return quantized_out, all_indices, all_losses
 
     def vq2emb(self, vq, proj=True):

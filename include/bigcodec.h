@@ -22,48 +22,49 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 1
+#define BC_ABI_VERSION 2
 
 int bc_abi_version(void);
 
-/* ---- Conv1d (weight-normed, optional fused SnakeBeta prologue / residual / tanh epilogue) ------
+/* ---- Conv1d (weight-normed, fused residual / tanh / next-Snake epilogue) --------------------------
  * Replaces: F.pad + conv1d of CausalConv1d.forward (vq/module.py:45-48) and weight_norm(nn.Conv1d)
- * (vq/module.py:59-65), preceded by Activation1d(SnakeBeta) (vq/alias_free_torch/act.py:25-32,
- * vq/activations.py:107-118) when snake_alpha_exp != NULL, followed by ResidualUnit's `x + ...`
- * (vq/module.py:88-89) when residual != NULL and by nn.Tanh (vq/codec_decoder.py:80) when
- * epilogue == 1.
- *   y[b,co,n] = bias[co] + sum_{ci,k} W[co,ci,k] * snake(x[b,ci, n*stride + k*dilation - pad_left])
- * with out-of-range input samples read as 0 (zero padding).  Non-causal: pad_left = padding;
- * causal: pad_left = (K - stride) * dilation (vq/module.py:43).
- * W is the FOLDED weight g*v/||v|| packed by bc_conv1d_pack for tile config `cfg`
- * (cfg = bc_conv1d_select_cfg(Cout, Cin)).
- * snake_alpha_exp[c] = exp(alpha[c]); snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9). */
-int bc_conv1d_select_cfg(int Cout, int Cin);
+ * (vq/module.py:59-65), followed by ResidualUnit's `x + ...` (vq/module.py:88-89) when
+ * residual != NULL, by nn.Tanh (vq/codec_decoder.py:80) when epilogue == 1, and by the SnakeBeta of
+ * the NEXT Activation1d (vq/activations.py:107-118) when out_snake_alpha_exp != NULL:
+ *   v[b,co,n] = residual[b,co,n] + bias[co] + sum_{ci,k} W[co,ci,k] * x[b,ci, n*stride + k*dilation - pad_left]
+ *   y = snake_co(v) (y2 == NULL)   or   y = v, y2 = snake_co(v) (dual output)   or   y = v / tanh(v)
+ * Out-of-range input samples read as 0 (zero padding).  Non-causal: pad_left = padding; causal:
+ * pad_left = (K - stride) * dilation (vq/module.py:43).  The input x is the already-activated
+ * tensor (the Snake that precedes every reference conv runs in the producer's epilogue or in
+ * bc_snake_fwd).  W is the FOLDED weight g*v/||v|| [Cout][Cin][K] packed by bc_conv1d_pack for
+ * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation).
+ * out_snake_alpha_exp[c] = exp(alpha[c]); out_snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9).
+ * Limits: Cin*Tin*4 < 2^31 bytes per clip. */
+int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation);
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg);
 int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg);
-int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias,
-                  const float* snake_alpha_exp, const float* snake_inv_beta,
-                  const float* residual, float* y,
-                  int B, int Cin, int Tin, int Cout, int Tout,
+int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, const float* residual,
+                  const float* out_snake_alpha_exp, const float* out_snake_inv_beta,
+                  float* y, float* y2, int B, int Cin, int Tin, int Cout, int Tout,
                   int K, int stride, int dilation, int pad_left, int epilogue, int cfg,
                   void* stream);
 
-/* ---- ConvTranspose1d (weight-normed, optional fused SnakeBeta prologue) ------------------------
+/* ---- ConvTranspose1d (weight-normed, fused next-Snake epilogue) -------------------------------
  * Replaces: weight_norm(nn.ConvTranspose1d) (vq/module.py:67-72) and CausalConvTranspose1d
  * (vq/module.py:50-57, crop of the last `stride` samples) inside DecoderBlock (vq/module.py:
  * 115-141) (DecoderBlock uses K = 2*stride).  Run as `stride` polyphase convolutions with
  * Kp = bc_convT1d_phase_taps(K, stride) = ceil(K/stride) taps: phase r has
  * W_r[co][ci][j'] = W[ci][co][r + stride*(Kp-1-j')] (0 where that tap index >= K), packed with
- * bc_conv1d_pack(..., K=Kp, cfg).  w_phases is a HOST array of `stride` device pointers.
- * Output length Tout = (Tin-1)*stride - 2*padding + K + output_padding (the caller passes Tout,
- * which carries output_padding); DecoderBlock non-causal: padding = stride/2 + stride%2,
- * output_padding = stride%2.  Causal (crop of the last `stride` samples): padding = 0,
- * Tout = (Tin-1)*stride + K - stride. */
+ * bc_conv1d_pack(..., K=Kp, cfg), cfg = bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1).  w_phases is
+ * a HOST array of `stride` device pointers.  Output length Tout = (Tin-1)*stride - 2*padding + K +
+ * output_padding (the caller passes Tout, which carries output_padding); DecoderBlock non-causal:
+ * padding = stride/2 + stride%2, output_padding = stride%2.  Causal (crop of the last `stride`
+ * samples): padding = 0, Tout = (Tin-1)*stride + K - stride.  Epilogue as bc_conv1d_fwd. */
 int bc_convT1d_phase_taps(int K, int stride);
 int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bias,
-                   const float* snake_alpha_exp, const float* snake_inv_beta, float* y,
-                   int B, int Cin, int Tin, int Cout, int Tout, int K, int stride, int padding,
-                   int cfg, void* stream);
+                   const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
+                   float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+                   int padding, int cfg, void* stream);
 
 /* ---- SnakeBeta / anti-aliased Activation1d -------------------------------------------------------
  * bc_snake_fwd replaces SnakeBeta.forward (vq/activations.py:107-118).
@@ -81,15 +82,18 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
  * Replaces ResLSTM.forward (vq/module.py:156-167): rearrange b f t -> b t f, nn.LSTM(H, H,
  * num_layers, batch_first=True) (unidirectional), + skip, rearrange back.  x, out: [B][H][T].
  * Per layer l: w_ih_packed[l] = bc_conv1d_pack(weight_ih_l{l} as [4H][H][1], cfg =
- * bc_conv1d_select_cfg(4H, H)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
+ * bc_conv1d_select_cfg(4H, H, 1, 1, 1)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
  * w_hh_packed[l] = bc_lstm_pack_hh(weight_hh_l{l}).  The three pointer arrays are HOST arrays of
- * device pointers.  workspace: bc_lstm_workspace_floats(B, H, T) device floats.  H % 16 == 0. */
+ * device pointers.  out = snake(y + x) when out_snake_alpha_exp != NULL (the Activation1d that
+ * follows the ResLSTM in both stacks), else y + x.  workspace: bc_lstm_workspace_floats(B, H, T)
+ * device floats.  H % 16 == 0. */
 long long bc_lstm_hh_packed_floats(int H);
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H);
 long long bc_lstm_workspace_floats(int B, int H, int T);
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
-                   const float* const* w_hh_packed, float* workspace, void* stream);
+                   const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                   const float* out_snake_inv_beta, float* workspace, void* stream);
 
 /* ---- Factorized VQ (codebook_dim == 8) ---------------------------------------------------------
  * bc_vq_prepare_codebook: F.normalize(codebook) and its row sums of squares

@@ -26,7 +26,7 @@ def test_library_loads_and_exports_all_declared_symbols():
         assert hasattr(lib, s), s
         assert s in L.EXPORTED, f"{s} missing from the ctypes signature table"
     assert set(L.EXPORTED) == set(syms)
-    assert lib.bc_abi_version() == 1
+    assert lib.bc_abi_version() == L.ABI_VERSION
 
 
 def test_library_is_gfx950_code_object():
@@ -39,7 +39,7 @@ def test_library_is_gfx950_code_object():
 @pytest.mark.parametrize("Cout,Cin,K", [(48, 1, 7), (48, 48, 7), (96, 48, 4), (1536, 768, 10), (1, 32, 7), (6144, 1536, 1)])
 def test_conv_pack_layout(Cout, Cin, K):
     lib = L.load()
-    cfg = lib.bc_conv1d_select_cfg(Cout, Cin)
+    cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, 1)
     mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
     n = lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg)
     bm = 16 * mt * wm
@@ -78,9 +78,12 @@ def test_lstm_pack_layout():
 
 def test_bad_arguments_are_rejected_without_launching():
     lib = L.load()
-    assert lib.bc_conv1d_select_cfg(0, 4) == -1
+    assert lib.bc_conv1d_select_cfg(0, 4, 7, 1, 1) == -1
     assert lib.bc_conv1d_packed_floats(8, 8, 0, 0) == -1
-    assert lib.bc_conv1d_fwd(None, None, None, None, None, None, None, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4, None) == 1
+    assert lib.bc_conv1d_fwd(None, None, None, None, None, None, None, None, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4,
+                             None) == 1
+    # dual output without an epilogue Snake, tanh together with a Snake: rejected
+    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, 1, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4, None) == 1
     assert lib.bc_lstm_hh_packed_floats(10) == -1
     assert lib.bc_vq_prepare_codebook(1, 1, 1, 8192, 16, None) == 3
     assert lib.bc_synth_clips(None, 1, 10, 0, None) == 1

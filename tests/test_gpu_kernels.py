@@ -6,6 +6,8 @@ import torch
 import torch.nn.functional as F
 
 from audiotokenization_amd import _lib as L
+from audiotokenization_amd import blocks as BL
+from audiotokenization_amd import conv as CV
 from audiotokenization_amd import modules as M
 from helpers import assert_close_rel
 from oracle import bigcodec_oracle as O
@@ -16,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def _rand_wn_conv(m, g, transposed=False):
     with torch.no_grad():
-        conv = m.conv if hasattr(m, "conv") and not isinstance(m, (M.Conv1dWN, M.ConvTranspose1dWN)) else m
+        conv = m.conv if hasattr(m, "conv") and not isinstance(m, (CV.Conv1dWN, CV.ConvTranspose1dWN)) else m
         conv.weight_v.copy_(torch.randn(conv.weight_v.shape, generator=g) / np.sqrt(np.prod(conv.weight_v.shape[1:])))
         conv.weight_g.copy_(torch.rand(conv.weight_g.shape, generator=g) + 0.5)
         conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
@@ -45,7 +47,8 @@ CONV_CASES = [
     (384, 768, 10, 5, 1, False, True, False, False, 1, 605),
     (192, 192, 7, 1, 9, False, True, False, False, 2, 300),
     (1536, 1024, 3, 1, 1, False, True, False, False, 2, 50),
-    (32, 1, 7, 1, 1, False, True, False, True, 2, 500),
+    (32, 1, 7, 1, 1, False, False, False, True, 2, 500),
+    (32, 1, 7, 1, 1, False, True, True, False, 2, 500),
     (20, 36, 5, 1, 2, False, True, True, False, 2, 64),
     (8, 8, 7, 1, 1, False, False, False, False, 1, 3),
 ]
@@ -56,25 +59,34 @@ def test_conv1d(dev, case):
     Cin, Cout, K, s, d, causal, use_snake, use_res, use_tanh, B, T = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     pad = 0 if causal else (K // 2 * d if s == 1 else s // 2 + s % 2)
-    m = M.WNConv1d(Cin, Cout, kernel_size=K, stride=s, dilation=d, padding=pad, causal=causal)
+    m = CV.WNConv1d(Cin, Cout, kernel_size=K, stride=s, dilation=d, padding=pad, causal=causal)
     conv = _rand_wn_conv(m, g)
     x = torch.randn(B, Cin, T, generator=g)
-    snake = _snake(Cin, g) if use_snake else None
+    snake = _snake(Cout, g) if use_snake else None  # the NEXT Activation1d, fused in the epilogue
     # CPU reference (oracle leaf ops)
     sd = {("conv." if causal else "") + k: v.detach() for k, v in conv.state_dict().items()}
-    xin = O.snake_beta(x, snake.alpha.detach(), snake.beta.detach()) if use_snake else x
-    want = O.conv(xin, sd, "", K, s, pad, d, causal)
+    want = O.conv(x, sd, "", K, s, pad, d, causal)
     res = torch.randn(want.shape, generator=g) if use_res else None
     if use_res:
         want = res + want
     if use_tanh:
         want = torch.tanh(want)
     m.to(dev)
+    tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64))
     co = snake.to(dev).coeffs(dev) if use_snake else None
-    got = m.run(x.to(dev), snake=co, residual=res.to(dev) if use_res else None, epilogue=int(use_tanh))
+    rd = res.to(dev) if use_res else None
+    got = m.run(x.to(dev), residual=rd, epilogue=int(use_tanh), out_snake=co)
     torch.cuda.synchronize()
     assert got.shape == want.shape
-    assert_close_rel(got.cpu(), want, 3e-6 * max(1.0, np.sqrt(Cin * K / 64)), f"conv {case}")
+    if use_snake:
+        want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
+        assert_close_rel(got.cpu(), want_s, tol * 4, f"conv+snake {case}")
+        raw, act = m.run(x.to(dev), residual=rd, out_snake=co, dual=True)
+        torch.cuda.synchronize()
+        assert_close_rel(raw.cpu(), want, tol, f"conv dual raw {case}")
+        assert torch.equal(act, got)
+    else:
+        assert_close_rel(got.cpu(), want, tol, f"conv {case}")
 
 
 CONVT_CASES = [
@@ -95,30 +107,47 @@ def test_conv_transpose1d(dev, case):
     g = torch.Generator().manual_seed(7 + s)
     K = 2 * s if s != 1 else 1
     kw = {} if causal else {"padding": s // 2 + s % 2 if s != 1 else 0, "output_padding": s % 2 if s != 1 else 0}
-    m = M.WNConvTranspose1d(Cin, Cout, kernel_size=K, stride=s, causal=causal, **kw)
+    m = CV.WNConvTranspose1d(Cin, Cout, kernel_size=K, stride=s, causal=causal, **kw)
     conv = _rand_wn_conv(m, g)
     x = torch.randn(B, Cin, T, generator=g)
-    snake = _snake(Cin, g) if use_snake else None
-    xin = O.snake_beta(x, snake.alpha.detach(), snake.beta.detach()) if use_snake else x
+    snake = _snake(Cout, g) if use_snake else None
     sd = {("conv." if causal else "") + k: v.detach() for k, v in conv.state_dict().items()}
     if s == 1:
-        want = F.conv_transpose1d(xin, O.wn_weight(sd, ""), sd["bias"], 1, 0, 0)
+        want = F.conv_transpose1d(x, O.wn_weight(sd, ""), sd["bias"], 1, 0, 0)
     else:
-        want = O.conv_transpose(xin, sd, "", s, causal)
+        want = O.conv_transpose(x, sd, "", s, causal)
     m.to(dev)
-    co = snake.to(dev).coeffs(dev) if use_snake else None
-    got = m.run(x.to(dev), snake=co)
+    got = m.run(x.to(dev))
     torch.cuda.synchronize()
     assert got.shape == want.shape
     assert_close_rel(got.cpu(), want, 1e-5, f"convT {case}")
+    if use_snake:
+        co = snake.to(dev).coeffs(dev)
+        raw, act = m.run(x.to(dev), out_snake=co, dual=True)
+        torch.cuda.synchronize()
+        assert torch.equal(raw, got)
+        want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
+        assert_close_rel(act.cpu(), want_s, 4e-5, f"convT snake {case}")
 
 
-def test_snake(dev):
+@pytest.mark.parametrize("scale", [3.0, 300.0, 20000.0, 1e6])
+def test_snake(dev, scale):
+    """SnakeBeta against the torch CPU expression and an fp64 evaluation, from small to huge
+    arguments (|x*alpha| >= 39000 takes the sinf fallback)."""
     g = torch.Generator().manual_seed(3)
     s = _snake(24, g)
-    x = torch.randn(3, 24, 1001, generator=g) * 3
+    x = torch.randn(3, 24, 1001, generator=g) * scale
     want = O.snake_beta(x, s.alpha.detach(), s.beta.detach())
     got = s.to(dev)(x.to(dev)).cpu()
+    a = torch.exp(s.alpha.detach().cpu().double())[None, :, None]
+    ib = (1.0 / (torch.exp(s.beta.detach().cpu()) + 1e-9)).double()[None, :, None]
+    t = (x.double() * a.float().double())  # the fp32 product, as the kernel forms it
+    t = (x * a.float()).double()
+    exact = x.double() + ib * torch.sin(t) ** 2
+    ulp = torch.finfo(torch.float32).eps * exact.abs().clamp_min(1e-30)
+    err_ulps = ((got.double() - exact).abs() / ulp).max().item()
+    cpu_ulps = ((want.double() - exact).abs() / ulp).max().item()
+    assert err_ulps <= max(8.0, 2 * cpu_ulps), (err_ulps, cpu_ulps)
     assert_close_rel(got, want, 2e-6, "snake")
 
 
@@ -136,7 +165,7 @@ def test_aa_activation(dev, golden):
 @pytest.mark.parametrize("H,layers,B,T", [(64, 2, 3, 50), (512, 1, 2, 20), (128, 2, 70, 9), (1536, 2, 2, 6)])
 def test_reslstm(dev, H, layers, B, T):
     g = torch.Generator().manual_seed(H + T)
-    m = M.ResLSTM(H, num_layers=layers)
+    m = BL.ResLSTM(H, num_layers=layers)
     with torch.no_grad():
         for p in m.lstm.parameters():
             p.copy_((torch.rand(p.shape, generator=g) * 2 - 1) / np.sqrt(H))
@@ -145,6 +174,11 @@ def test_reslstm(dev, H, layers, B, T):
     want = O.res_lstm(x, sd, "", layers)
     got = m.to(dev)(x.to(dev)).cpu()
     assert_close_rel(got, want, 2e-5, f"lstm H={H}")
+    # fused output Snake (the Activation1d after the ResLSTM)
+    snake = _snake(H, g).to(dev)
+    got_s = m.run(x.to(dev), out_snake=snake.coeffs(dev)).cpu()
+    want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
+    assert_close_rel(got_s, want_s, 5e-5, f"lstm+snake H={H}")
 
 
 def test_vq_argmin_bit_exact(dev, golden):
@@ -231,5 +265,5 @@ def test_synth_clips_device_equals_host(dev):
 def test_abi_rejects_bad_args(dev):
     lib = L.load()
     # wrong cfg for the shape -> BC_ERR_ARG, nothing launched
-    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 0, None) == 1
+    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 0, None) == 1
     assert lib.bc_vq_argmin(1, 1, 1, 1, 10, 8192, 4, None) == 3
