@@ -189,8 +189,10 @@ static const int kBKC[] = {32, 16, 8, 4};
 static int stage_budget() {
   static int v = [] {
     const char* e = getenv("BC_STAGE_BUDGET_KB");
-    const int kb = e ? atoi(e) : 40;
-    return (kb >= 8 && kb <= 78 ? kb : 40) * 1024;
+    // 32 KB measured best on MI355X (profiles/r01_stage_budget_sweep.txt: 16/24/32/40/56 KB ->
+    // 568/562/561/603/698 ms per config-2 step): 2 stages x 32 KB keeps 2 workgroups per CU.
+    const int kb = e ? atoi(e) : 32;
+    return (kb >= 8 && kb <= 78 ? kb : 32) * 1024;
   }();
   return v;
 }
