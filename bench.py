@@ -63,6 +63,20 @@ def build_model(name, device):
     return enc, dec, sds, ek, dk
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (tools/gpu_pmc.sh ->
+    tools/pmc_summary.py -> profiles/*pmc_traffic.json), or (None, None)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))["kernels"].get(kernel)
+    if not d:
+        return None, None
+    return d["traffic_bytes_corrected"], os.path.basename(files[-1])
+
+
 def cpu_baseline(name, n_samples, sds, ek, dk, n_clips):
     """The CPU oracle (torch CPU restatement, bit-identical to the reference in the development
     container) timed on this host: encode + VQ, B = 1 per clip (extract_indices.py:397), warm run."""
@@ -149,8 +163,11 @@ def main():
         avg_ms = d["ms_total"] / d["launches"]
         achieved = d["flops_total"] / d["launches"] / (avg_ms * 1e-3) / 1e12
         conv_ms = sum(v["ms_total"] for v in summ.values())
+        traffic, tsrc = pmc_traffic(kname)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None, "kernel": kname,
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+                "algorithmic_bytes_per_launch": round(d["bytes_total"] / d["launches"]), "kernel": kname,
                 "launches_per_step": d["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_gflop_per_launch": round(d["flops_total"] / d["launches"] / 1e9, 3),
                 "all_python_conv_kernels_ms_per_step": round(conv_ms / args.steps, 2),
