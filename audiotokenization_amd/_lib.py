@@ -22,7 +22,7 @@ L = C.c_longlong
 # name -> (restype, argtypes)
 _SIGS = {
     "bc_abi_version": (I, []),
-    "bc_conv1d_select_cfg": (I, [I, I, I, I, I]),
+    "bc_conv1d_select_cfg": (I, [I, I, I, I, I, I]),
     "bc_conv1d_packed_floats": (L, [I, I, I, I]),
     "bc_conv1d_pack": (I, [P, P, I, I, I, I]),
     "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
@@ -33,7 +33,7 @@ _SIGS = {
     "bc_lstm_hh_packed_floats": (L, [I]),
     "bc_lstm_pack_hh": (I, [P, P, I]),
     "bc_lstm_workspace_floats": (L, [I, I, I]),
-    "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, P]),
+    "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
     "bc_vq_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P]),
     "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
@@ -165,9 +165,40 @@ _BKC = [32, 16, 8, 4]
 CONV_CFGS = {t * 4 + b: _TILES[t] + (_BKC[b],) for t in range(5) for b in range(4)}
 
 
+# csrc/conv1d_x6.hip kX6Tiles (cfg = 100 + index) -> (MT, NT, WM, WN)
+X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 4, 2), (2, 2, 4, 2), (6, 2, 1, 8),
+                                              (4, 2, 1, 8), (3, 2, 1, 8), (2, 2, 1, 8), (1, 2, 1, 8), (6, 1, 1, 8),
+                                              (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8)])}
+
+
 def conv_kernel_name(cfg: int) -> str:
+    if cfg in X6_CFGS:
+        mt, nt, wm, wn = X6_CFGS[cfg]
+        return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
+
+
+# Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6",
+# the default: same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling).
+PRECISIONS = {"fp32": 0, "x6": 1}
+_mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "x6")]
+
+
+def set_precision(name: str) -> None:
+    """Select the conv GEMM arithmetic ('fp32' or 'x6'); prepared weights re-pack on next use."""
+    global _mode
+    if name not in PRECISIONS:
+        raise ValueError(f"unknown precision {name!r}: expected one of {sorted(PRECISIONS)}")
+    _mode = PRECISIONS[name]
+
+
+def precision_mode() -> int:
+    return _mode
+
+
+def precision_name() -> str:
+    return {v: k for k, v in PRECISIONS.items()}[_mode]
 
 
 def ptr_array(ptrs):

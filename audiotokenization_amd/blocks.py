@@ -191,7 +191,7 @@ class LSTM(nn.Module):
             H = self.hidden_size
             if self.input_size != H:
                 raise NotImplementedError("ResLSTM requires input_size == hidden_size")
-            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1)
+            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1, L.precision_mode())
             wih, whh, bias = [], [], []
             for l in range(self.num_layers):
                 w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
@@ -207,7 +207,7 @@ class LSTM(nn.Module):
             arrs = (L.ptr_array([t.data_ptr() for t in wih]), L.ptr_array([t.data_ptr() for t in bias]),
                     L.ptr_array([t.data_ptr() for t in whh]))
             return (wih, whh, bias), arrs
-        return self._cache.get(_pkey(*self._plist()) + (str(device),), build)
+        return self._cache.get(_pkey(*self._plist()) + (str(device), L.precision_mode()), build)
 
 
 class ResLSTM(nn.Module):
@@ -230,7 +230,7 @@ class ResLSTM(nn.Module):
         y = torch.empty_like(x)
         sa, sb = out_snake if out_snake is not None else (None, None)
         L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
-               L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.stream_of(x))
+               L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.stream_of(x))
         return y
 
     def flow(self, x_raw, want_raw=True, next_act=None) -> Flow:

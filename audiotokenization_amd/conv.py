@@ -89,12 +89,12 @@ class Conv1dWN(_WNParams, nn.Module):
             w = self.folded_weight().contiguous()
             Cout, Cin, K = w.shape
             lib = L.load()
-            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, self.stride, self.dilation)
+            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, self.stride, self.dilation, L.precision_mode())
             packed = np.empty(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg), dtype=np.float32)
             L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, Cout, Cin, K, cfg)
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return torch.from_numpy(packed).to(device), bias, cfg
-        return self._cache.get(_pkey(*self._params()) + (str(device),), build)
+        return self._cache.get(_pkey(*self._params()) + (str(device), L.precision_mode()), build)
 
     def pad_left(self) -> int:
         return self.causal_pad if self.causal_pad is not None else self.padding
@@ -194,7 +194,7 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
             s = self.stride
             lib = L.load()
             Kp = lib.bc_convT1d_phase_taps(K, s)
-            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1)
+            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1, L.precision_mode())
             n = lib.bc_conv1d_packed_floats(Cout, Cin, Kp, cfg)
             wt = w.permute(1, 0, 2).contiguous()  # (Cout, Cin, K)
             phases = []
@@ -209,7 +209,7 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
                 phases.append(torch.from_numpy(packed).to(device))
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return phases, L.ptr_array([p.data_ptr() for p in phases]), bias, cfg
-        return self._cache.get(_pkey(*self._params()) + (str(device),), build)
+        return self._cache.get(_pkey(*self._params()) + (str(device), L.precision_mode()), build)
 
     def out_len(self, T: int) -> int:
         full = (T - 1) * self.stride - 2 * self.padding + self.kernel_size + self.output_padding

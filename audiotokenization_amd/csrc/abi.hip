@@ -11,9 +11,15 @@ extern "C" {
 
 int bc_abi_version(void) { return BC_ABI_VERSION; }
 
-int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation) {
+int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode) {
   if (Cout <= 0 || Cin <= 0 || K <= 0 || stride <= 0 || dilation <= 0) return -1;
-  return conv_select_cfg(Cout, Cin, K, stride, dilation);
+  if (mode != 0 && mode != 1) return -1;
+  return conv_select_cfg(Cout, Cin, K, stride, dilation, mode);
+}
+
+// a cfg is acceptable for a shape if either precision mode selects it
+static bool cfg_matches(int cfg, int Cout, int Cin, int K, int s, int d) {
+  return cfg == conv_select_cfg(Cout, Cin, K, s, d, 0) || cfg == conv_select_cfg(Cout, Cin, K, s, d, 1);
 }
 
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg) {
@@ -39,7 +45,7 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
   if (epilogue != 0 && epilogue != 1) return BC_ERR_ARG;
   if (epilogue == 1 && out_snake_alpha_exp) return BC_ERR_ARG;
-  if (cfg != conv_select_cfg(Cout, Cin, K, stride, dilation)) return BC_ERR_ARG;
+  if (!cfg_matches(cfg, Cout, Cin, K, stride, dilation)) return BC_ERR_ARG;
   if (B == 0 || Tout == 0) return BC_OK;
   ConvArgs a{};
   a.x = x; a.w = w_packed; a.bias = bias; a.res = residual;
@@ -67,7 +73,7 @@ int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bi
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
   const int s = stride, p = padding;
   const int Kp = (K + s - 1) / s;  // taps per phase
-  if (cfg != conv_select_cfg(Cout, Cin, Kp, 1, 1)) return BC_ERR_ARG;
+  if (!cfg_matches(cfg, Cout, Cin, Kp, 1, 1)) return BC_ERR_ARG;
   if (B == 0 || Tout == 0) return BC_OK;
   for (int r = 0; r < s; ++r) {
     if (!w_phases[r]) return BC_ERR_ARG;
@@ -135,9 +141,9 @@ long long bc_lstm_workspace_floats(int B, int H, int T) {
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
-                   const float* out_snake_inv_beta, float* workspace, void* stream) {
+                   const float* out_snake_inv_beta, float* workspace, int mode, void* stream) {
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
-      H % 16 || T < 0 || num_layers <= 0)
+      H % 16 || T < 0 || num_layers <= 0 || (mode != 0 && mode != 1))
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
@@ -153,7 +159,7 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
   const bool fast = lstm_fast_ok(H);
   int rc = btc_to_ctb_launch(x, xt, B, H, T, st);
   if (rc) return rc;
-  const int cfg = conv_select_cfg(4 * H, H, 1, 1, 1);
+  const int cfg = conv_select_cfg(4 * H, H, 1, 1, 1, mode);
   const float* lin = xt;
   float* lout = ya;
   for (int l = 0; l < num_layers; ++l) {

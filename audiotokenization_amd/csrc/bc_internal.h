@@ -22,8 +22,15 @@ struct ConvArgs {
   float inv_win;
   int ntm, ntn, nwg;
 };
-int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation);
+// mode 0: fp32 MFMA kernel (cfg 0..19); mode 1: fp32-accurate 3xbf16 kernel (cfg 100..) where the
+// shape suits it, else the fp32 kernel.
+int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode = 0);
 bool conv_cfg_valid(int cfg_id);
+int x6_select_cfg(int Cout, int Cin, int K, int s, int d);
+bool x6_cfg_valid(int cfg);
+long long x6_packed_bytes(int Cout, int Cin, int K, int cfg);
+void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg);
+int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st);
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id);
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id);
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);

@@ -233,7 +233,11 @@ static Geometry geometry(const Tile& t, int bkc, int K, int s, int d) {
   return g;
 }
 
-int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation) {
+int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode) {
+  if (mode == 1) {
+    const int c = x6_select_cfg(Cout, Cin, K, stride, dilation);
+    if (c >= 0) return c;
+  }
   int tile;
   if (Cout >= 128) tile = 0;
   else if (Cout > 48) tile = 1;
@@ -251,9 +255,10 @@ int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation) {
   return tile * 4 + 3;  // BKC = 4 always fits the shapes the codec builds
 }
 
-bool conv_cfg_valid(int cfg_id) { return cfg_id >= 0 && cfg_id < 20; }
+bool conv_cfg_valid(int cfg_id) { return (cfg_id >= 0 && cfg_id < 20) || x6_cfg_valid(cfg_id); }
 
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id) {
+  if (x6_cfg_valid(cfg_id)) return x6_packed_bytes(Cout, Cin, K, cfg_id) / 4;
   const Tile& t = kTiles[cfg_id / 4];
   const int bkc = kBKC[cfg_id % 4];
   const int ntm = (Cout + tile_BM(t) - 1) / tile_BM(t);
@@ -266,6 +271,10 @@ long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id) {
 // Layout: [mgroup][chunk][kstep][lane][4]; mgroup = 16*MT output rows; element i of the float4 is
 // m-tile i (zero for i >= MT); lane -> (row = lane&15, k = 4*kstep + (lane>>4)), k tap-major.
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id) {
+  if (x6_cfg_valid(cfg_id)) {
+    x6_pack_weight(w, reinterpret_cast<unsigned short*>(out), Cout, Cin, K, cfg_id);
+    return;
+  }
   const Tile& t = kTiles[cfg_id / 4];
   const int bkc = kBKC[cfg_id % 4];
   const int ntm = (Cout + tile_BM(t) - 1) / tile_BM(t);
@@ -321,6 +330,7 @@ static int launch_tile(ConvArgs& a, int B, hipStream_t st) {
   case T * 4 + 3: return launch_tile<MT, WM, NT, WN, 4>(a, B, st);
 
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st) {
+  if (x6_cfg_valid(cfg_id)) return x6_launch(a, B, cfg_id, st);
   switch (cfg_id) {
     BC_TILE_CASES(0, 4, 2, 4, 2)
     BC_TILE_CASES(1, 4, 1, 4, 4)

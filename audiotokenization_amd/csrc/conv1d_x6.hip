@@ -1,0 +1,374 @@
+// Conv1d with fp32-accurate "3 x bf16" MFMA (x6 mode) for gfx950.
+//
+// Same GEMM and epilogue as conv1d.hip (reference: vq/module.py:11-72 and its callers), but the
+// products run on v_mfma_f32_16x16x32_bf16 (16x the fp32 MFMA rate) with every fp32 operand split
+// EXACTLY into three bf16 terms, v = v0 + v1 + v2 (round-to-nearest splits; 8+8+8 significant bits
+// hold all 24 of an fp32 mantissa).  a*b is accumulated as the six terms with i+j <= 2:
+//   a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0
+// Every bf16*bf16 product is exact in fp32 and the MFMA accumulates in fp32; the three dropped terms
+// are below 2^-26 |ab|.  The result has fp32-level error (DESIGN.md §4 measures it against fp64
+// next to native fp32 accumulation) at 6/16 of the fp32-MFMA cost.
+//
+// Workgroup: 512 threads = WM x WN waves, each MT x NT 16x16 tiles; BM = 16*MT*WM, BN = 16*NT*WN.
+// K is walked per (32-channel chunk, tap) = one K32 step.
+//   A (weights): split and packed on the host, [mgroup][chunk][tap][plane][m-tile][lane][8 bf16];
+//                one step's block (3 planes x WM*MT KiB) is copied by LDS-DMA, double-buffered.
+//   B (input)  : per chunk, rows of the tile (incl. stride/dilation halo) are read from HBM into
+//                registers (buffer loads: out-of-range -> 0), split into 3 bf16 planes and written
+//                channel-contiguous ([col][32 ch], 80-B pitch: conflict-free b128 reads at stride 1)
+//                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
+//                at tap 0 and land while the current chunk's taps compute.
+#include <cstring>
+
+#include "bc_common.h"
+#include "bc_internal.h"
+
+namespace bc {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
+constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
+constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352
+
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2_t v = __builtin_convertvector((float2_t){a, b}, bf16x2_t);
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+template <int MT, int NT, int WM, int WN>
+__global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
+  constexpr int BM = 16 * MT * WM;
+  constexpr int BN = 16 * NT * WN;
+  constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
+
+  const int ncol = a.win;                // columns of the input tile
+  const int bplane = a.bstage;           // bytes per B plane (multiple of 16)
+  unsigned char* Bs = smem_x6;                            // [3][ncol][80 B]
+  unsigned char* As = smem_x6 + 3 * bplane;               // [2][3][QA][1 KiB]
+
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int mt_idx = wg % a.ntm;
+  const int rest = wg / a.ntm;
+  const int nt_idx = rest % a.ntn;
+  const int b = rest / a.ntn;
+  const int m0 = mt_idx * BM;
+  const int n0 = nt_idx * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+
+  const unsigned long long xb_u = (unsigned long long)(a.x + (long long)b * a.xbs);
+  const unsigned xb_lo = __builtin_amdgcn_readfirstlane((unsigned)xb_u);
+  const unsigned xb_hi = __builtin_amdgcn_readfirstlane((unsigned)(xb_u >> 32));
+  const int xbytes = __builtin_amdgcn_readfirstlane(a.Cin * a.Tin * 4);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long long)xb_hi << 32) | xb_lo), 0, xbytes, 0x00020000);
+  const int in0 = n0 * a.s - a.pl;
+
+  const int K = a.K;
+  const int nsteps = a.nchunks * K;
+  const int a_pieces = 3 * QA;
+  const unsigned char* wblk = reinterpret_cast<const unsigned char*>(a.w) +
+                              (long long)mt_idx * a.nchunks * K * (a_pieces * 1024);
+
+  auto issue_a = [&](int step, int buf) {
+    const unsigned char* src = wblk + (long long)step * (a_pieces * 1024);
+    unsigned char* dst = As + buf * (a_pieces * 1024);
+    for (int q = wave; q < a_pieces; q += 8)
+      __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
+                                       16, 0, 0);
+  };
+
+  // B staging: thread -> (channel pair p, column lane cl); columns cl + 32*i
+  const int bp = tid >> 5;       // 0..15
+  const int bcl = tid & 31;
+  float bv0[X6_MAXCOL_ITERS], bv1[X6_MAXCOL_ITERS];
+  auto load_b = [&](int chunk) {
+    const int ci0 = chunk * X6_BKC + 2 * bp;
+#pragma unroll
+    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+      const int col = bcl + 32 * i;
+      const int ti = in0 + col;
+      const bool tin = col < ncol && ti >= 0 && ti < a.Tin;
+      const unsigned o0 = (tin && ci0 < a.Cin) ? (unsigned)((ci0 * a.Tin + ti) * 4) : 0xfffffff0u;
+      const unsigned o1 = (tin && ci0 + 1 < a.Cin) ? (unsigned)(((ci0 + 1) * a.Tin + ti) * 4) : 0xfffffff0u;
+      bv0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
+      bv1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
+    }
+  };
+  auto store_b = [&]() {
+#pragma unroll
+    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+      const int col = bcl + 32 * i;
+      if (col < ncol) {
+        const float v0 = bv0[i], v1 = bv1[i];
+        const unsigned h = pk_bf16(v0, v1);
+        const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
+        const unsigned m = pk_bf16(r0, r1);
+        const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
+        const unsigned l = pk_bf16(s0, s1);
+        unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+        *reinterpret_cast<unsigned*>(p) = h;
+        *reinterpret_cast<unsigned*>(p + bplane) = m;
+        *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
+      }
+    }
+  };
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
+  const int kgrp16 = (lane >> 4) * 16;
+
+  // prologue: A(step 0), B(chunk 0)
+  issue_a(0, 0);
+  load_b(0);
+  store_b();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int c = 0; c < a.nchunks; ++c) {
+    for (int tap = 0; tap < K; ++tap) {
+      const int step = c * K + tap;
+      if (step + 1 < nsteps) issue_a(step + 1, (step + 1) & 1);
+      if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
+      const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
+      const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
+      bf16x8_t bf[NT][3];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[j][p] = *reinterpret_cast<const bf16x8_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
+        const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          floatx4 t = acc[i][j];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[j][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], t, 0, 0, 0);
+          acc[i][j] = t;
+        }
+      }
+      if (tap == K - 1 && c + 1 < a.nchunks) {
+        __syncthreads();  // every wave is done reading this chunk's B tile
+        store_b();
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (C/D layout of 16x16x32 == 16x16x4: col = lane&15, row = (lane>>4)*4 + r) -----
+  float* yb = a.y + (long long)b * a.ybs;
+  float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
+  const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m0 + wm * MT * 16 + i * 16 + (lane >> 4) * 4 + r;
+      if (co >= a.Cout) continue;
+      const float bias = a.bias ? a.bias[co] : 0.f;
+      const float sa = a.osa ? a.osa[co] : 0.f;
+      const float sb = a.osa ? a.osb[co] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn * NT * 16 + j * 16 + (lane & 15);
+        if (n >= a.Nout) continue;
+        const long long yi = (long long)co * a.yT + (long long)n * a.ostride + a.ooff;
+        float v = acc[i][j][r] + bias;
+        if (rb) v = rb[yi] + v;
+        if (a.epi == 1) v = tanhf(v);
+        if (a.osa) {
+          const float sv = snake(v, sa, sb);
+          if (y2b) {
+            yb[yi] = v;
+            y2b[yi] = sv;
+          } else {
+            yb[yi] = sv;
+          }
+        } else {
+          yb[yi] = v;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+struct X6Tile {
+  int MT, NT, WM, WN;
+};
+// cfg ids 100..: index into this table
+static const X6Tile kX6Tiles[] = {
+    {4, 4, 2, 4},  // 100: BM=128 BN=256  (Cout >= 128, stride 1)
+    {4, 2, 2, 4},  // 101: BM=128 BN=128  (Cout >= 128, stride 2)
+    {4, 2, 4, 2},  // 102: BM=256 BN=64   (Cout >= 256, stride >= 3)
+    {2, 2, 4, 2},  // 103: BM=128 BN=64   (Cout >= 128, stride >= 3)
+    {6, 2, 1, 8},  // 104: BM=96  BN=256
+    {4, 2, 1, 8},  // 105: BM=64  BN=256
+    {3, 2, 1, 8},  // 106: BM=48  BN=256
+    {2, 2, 1, 8},  // 107: BM=32  BN=256
+    {1, 2, 1, 8},  // 108: BM=16  BN=256
+    {6, 1, 1, 8},  // 109: BM=96  BN=128
+    {4, 1, 1, 8},  // 110: BM=64  BN=128
+    {3, 1, 1, 8},  // 111: BM=48  BN=128
+    {2, 1, 1, 8},  // 112: BM=32  BN=128
+    {1, 1, 1, 8},  // 113: BM=16  BN=128
+};
+constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
+
+static inline int x6_BM(const X6Tile& t) { return 16 * t.MT * t.WM; }
+static inline int x6_BN(const X6Tile& t) { return 16 * t.NT * t.WN; }
+static inline int x6_ncol(const X6Tile& t, int K, int s, int d) { return (x6_BN(t) - 1) * s + (K - 1) * d + 1; }
+static inline size_t x6_lds(const X6Tile& t, int ncol) {
+  const size_t bplane = (size_t)((ncol * X6_PITCH + 15) / 16 * 16);
+  return 3 * bplane + 2 * 3 * (size_t)t.WM * t.MT * 1024;
+}
+
+bool x6_cfg_valid(int cfg) { return cfg >= 100 && cfg < 100 + X6_NT; }
+
+// Returns a x6 cfg id, or -1 when the shape should stay on the fp32 kernel.
+int x6_select_cfg(int Cout, int Cin, int K, int s, int d) {
+  if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
+  int order[4];
+  int n = 0;
+  if (Cout >= 128) {
+    if (s == 1) order[n++] = 0;
+    if (s <= 2) order[n++] = 1;
+    if (Cout >= 256) order[n++] = 2;
+    order[n++] = 3;
+  } else {
+    const int mt = (Cout + 15) / 16;
+    const int base = mt == 6 || mt == 5 ? 0 : mt == 4 ? 1 : mt == 3 ? 2 : mt == 2 ? 3 : 4;
+    if (mt > 6) return -1;
+    order[n++] = 4 + base;
+    order[n++] = 9 + base;
+  }
+  for (int i = 0; i < n; ++i) {
+    const X6Tile& t = kX6Tiles[order[i]];
+    const int ncol = x6_ncol(t, K, s, d);
+    if (ncol > 32 * X6_MAXCOL_ITERS) continue;
+    if (x6_lds(t, ncol) > 160 * 1024) continue;
+    return 100 + order[i];
+  }
+  return -1;
+}
+
+long long x6_packed_bytes(int Cout, int Cin, int K, int cfg) {
+  const X6Tile& t = kX6Tiles[cfg - 100];
+  const int ntm = (Cout + x6_BM(t) - 1) / x6_BM(t);
+  const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
+  return (long long)ntm * nchunks * K * 3 * t.WM * t.MT * 1024;
+}
+
+static inline unsigned short f2bf_rn(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);  // NaN
+  const unsigned r = u + 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(r >> 16);
+}
+static inline float bf2f(unsigned short h) {
+  const unsigned u = (unsigned)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// w: [Cout][Cin][K] fp32 host -> packed bf16 planes (host), layout documented at the top.
+void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg) {
+  const X6Tile& t = kX6Tiles[cfg - 100];
+  const int BM = x6_BM(t), QA = t.WM * t.MT;
+  const int ntm = (Cout + BM - 1) / BM;
+  const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
+  long long o = 0;
+  for (int mg = 0; mg < ntm; ++mg)
+    for (int c = 0; c < nchunks; ++c)
+      for (int tap = 0; tap < K; ++tap)
+        for (int p = 0; p < 3; ++p)
+          for (int q = 0; q < QA; ++q)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int j = 0; j < 8; ++j, ++o) {
+                const int row = mg * BM + q * 16 + (lane & 15);
+                const int ci = c * X6_BKC + 8 * (lane >> 4) + j;
+                float v = 0.f;
+                if (row < Cout && ci < Cin) v = w[((long long)row * Cin + ci) * K + tap];
+                const unsigned short h0 = f2bf_rn(v);
+                const float r1 = v - bf2f(h0);
+                const unsigned short h1 = f2bf_rn(r1);
+                const float r2 = r1 - bf2f(h1);
+                const unsigned short h2 = f2bf_rn(r2);
+                out[o] = p == 0 ? h0 : p == 1 ? h1 : h2;
+              }
+}
+
+template <int MT, int NT, int WM, int WN>
+static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const X6Tile t{MT, NT, WM, WN};
+  const int ncol = x6_ncol(t, a.K, a.s, a.d);
+  if (ncol > 32 * X6_MAXCOL_ITERS) return BC_ERR_UNSUPPORTED;
+  a.ntm = (a.Cout + BM - 1) / BM;
+  a.ntn = (a.Nout + BN - 1) / BN;
+  a.nchunks = (a.Cin + X6_BKC - 1) / X6_BKC;
+  a.win = ncol;
+  a.bstage = (ncol * X6_PITCH + 15) / 16 * 16;
+  const long long nwg = (long long)a.ntm * a.ntn * B;
+  if (nwg <= 0) return BC_OK;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  a.nwg = (int)nwg;
+  const size_t lds = x6_lds(t, ncol);
+  if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN>), dim3(a.nwg), dim3(512), lds, st, a);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 100: return launch_x6<4, 4, 2, 4>(a, B, st);
+    case 101: return launch_x6<4, 2, 2, 4>(a, B, st);
+    case 102: return launch_x6<4, 2, 4, 2>(a, B, st);
+    case 103: return launch_x6<2, 2, 4, 2>(a, B, st);
+    case 104: return launch_x6<6, 2, 1, 8>(a, B, st);
+    case 105: return launch_x6<4, 2, 1, 8>(a, B, st);
+    case 106: return launch_x6<3, 2, 1, 8>(a, B, st);
+    case 107: return launch_x6<2, 2, 1, 8>(a, B, st);
+    case 108: return launch_x6<1, 2, 1, 8>(a, B, st);
+    case 109: return launch_x6<6, 1, 1, 8>(a, B, st);
+    case 110: return launch_x6<4, 1, 1, 8>(a, B, st);
+    case 111: return launch_x6<3, 1, 1, 8>(a, B, st);
+    case 112: return launch_x6<2, 1, 1, 8>(a, B, st);
+    case 113: return launch_x6<1, 1, 1, 8>(a, B, st);
+  }
+  return BC_ERR_ARG;
+}
+
+}  // namespace bc

@@ -37,10 +37,14 @@ int bc_abi_version(void);
  * pad_left = (K - stride) * dilation (vq/module.py:43).  The input x is the already-activated
  * tensor (the Snake that precedes every reference conv runs in the producer's epilogue or in
  * bc_snake_fwd).  W is the FOLDED weight g*v/||v|| [Cout][Cin][K] packed by bc_conv1d_pack for
- * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation).
+ * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode).
+ * mode 0: fp32 MFMA (v_mfma_f32_16x16x4_f32).  mode 1: fp32-accurate "x6" MFMA — both operands
+ * split exactly into three bf16 terms, six bf16 products per pair accumulated in fp32 — for the
+ * shapes where it applies (Cin >= 16), else the fp32 kernel.  Its error against fp64 is at or below
+ * the fp32 kernel's.
  * out_snake_alpha_exp[c] = exp(alpha[c]); out_snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9).
  * Limits: Cin*Tin*4 < 2^31 bytes per clip. */
-int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation);
+int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode);
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg);
 int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg);
 int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, const float* residual,
@@ -55,7 +59,7 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
  * 115-141) (DecoderBlock uses K = 2*stride).  Run as `stride` polyphase convolutions with
  * Kp = bc_convT1d_phase_taps(K, stride) = ceil(K/stride) taps: phase r has
  * W_r[co][ci][j'] = W[ci][co][r + stride*(Kp-1-j')] (0 where that tap index >= K), packed with
- * bc_conv1d_pack(..., K=Kp, cfg), cfg = bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1).  w_phases is
+ * bc_conv1d_pack(..., K=Kp, cfg), cfg = bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1, mode).  w_phases is
  * a HOST array of `stride` device pointers.  Output length Tout = (Tin-1)*stride - 2*padding + K +
  * output_padding (the caller passes Tout, which carries output_padding); DecoderBlock non-causal:
  * padding = stride/2 + stride%2, output_padding = stride%2.  Causal (crop of the last `stride`
@@ -82,7 +86,7 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
  * Replaces ResLSTM.forward (vq/module.py:156-167): rearrange b f t -> b t f, nn.LSTM(H, H,
  * num_layers, batch_first=True) (unidirectional), + skip, rearrange back.  x, out: [B][H][T].
  * Per layer l: w_ih_packed[l] = bc_conv1d_pack(weight_ih_l{l} as [4H][H][1], cfg =
- * bc_conv1d_select_cfg(4H, H, 1, 1, 1)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
+ * bc_conv1d_select_cfg(4H, H, 1, 1, 1, mode)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
  * w_hh_packed[l] = bc_lstm_pack_hh(weight_hh_l{l}).  The three pointer arrays are HOST arrays of
  * device pointers.  out = snake(y + x) when out_snake_alpha_exp != NULL (the Activation1d that
  * follows the ResLSTM in both stacks), else y + x.  workspace: bc_lstm_workspace_floats(B, H, T)
@@ -93,7 +97,7 @@ long long bc_lstm_workspace_floats(int B, int H, int T);
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
-                   const float* out_snake_inv_beta, float* workspace, void* stream);
+                   const float* out_snake_inv_beta, float* workspace, int mode, void* stream);
 
 /* ---- Factorized VQ (codebook_dim == 8) ---------------------------------------------------------
  * bc_vq_prepare_codebook: F.normalize(codebook) and its row sums of squares

@@ -38,6 +38,18 @@ def golden():
     return load_golden
 
 
+@pytest.fixture(params=["fp32", "x6"])
+def prec(request):
+    """Run a test under both conv GEMM precisions: native fp32 MFMA and the fp32-accurate 3xbf16
+    split MFMA (csrc/conv1d_x6.hip)."""
+    from audiotokenization_amd import _lib
+
+    old = _lib.precision_mode()
+    _lib.set_precision(request.param)
+    yield request.param
+    _lib._mode = old
+
+
 @pytest.fixture(scope="session")
 def dev():
     import torch

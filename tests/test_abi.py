@@ -39,7 +39,7 @@ def test_library_is_gfx950_code_object():
 @pytest.mark.parametrize("Cout,Cin,K", [(48, 1, 7), (48, 48, 7), (96, 48, 4), (1536, 768, 10), (1, 32, 7), (6144, 1536, 1)])
 def test_conv_pack_layout(Cout, Cin, K):
     lib = L.load()
-    cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, 1)
+    cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, 1, 0)
     mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
     n = lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg)
     bm = 16 * mt * wm
@@ -63,6 +63,41 @@ def test_conv_pack_layout(Cout, Cin, K):
     assert np.isclose(P.sum(dtype=np.float64), w.sum(dtype=np.float64), rtol=1e-6, atol=1e-3)
 
 
+def _bf16_to_f64(h):
+    return (h.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("Cout,Cin,K", [(48, 48, 7), (96, 48, 4), (1536, 768, 10), (6144, 1536, 1), (20, 36, 5)])
+def test_x6_pack_layout_and_exact_split(Cout, Cin, K):
+    """x6 mode packs each weight as three bf16 planes w = h0 + h1 + h2 (exact), in the
+    [mg][chunk][tap][plane][q][lane][8] order conv1d_x6.hip documents."""
+    lib = L.load()
+    cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, 1, 1)
+    assert cfg in L.X6_CFGS
+    mt, nt, wm, wn = L.X6_CFGS[cfg]
+    bm, qa = 16 * mt * wm, mt * wm
+    ntm, nch = -(-Cout // bm), -(-Cin // 32)
+    n = lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg)
+    assert n * 4 == ntm * nch * K * 3 * qa * 1024
+    rng = np.random.default_rng(1)
+    w = (rng.standard_normal((Cout, Cin, K)) * np.exp(rng.standard_normal((Cout, 1, 1)) * 3)).astype(np.float32)
+    out = np.empty(n, np.float32)
+    assert lib.bc_conv1d_pack(w.ctypes.data, out.ctypes.data, Cout, Cin, K, cfg) == 0
+    P = out.view(np.uint16).reshape(ntm, nch, K, 3, qa, 64, 8)
+    planes = _bf16_to_f64(P)
+    total = planes.sum(axis=3)  # (ntm, nch, K, qa, 64, 8)
+    for _ in range(300):
+        mg, c, tap, q, lane, j = (rng.integers(s) for s in total.shape)
+        row = mg * bm + q * 16 + (lane & 15)
+        ci = c * 32 + 8 * (lane >> 4) + j
+        want = float(w[row, ci, tap]) if (row < Cout and ci < Cin) else 0.0
+        assert total[mg, c, tap, q, lane, j] == want
+        # each plane is the bf16 rounding of the remainder of the previous ones (|h1| <= ulp_bf16(h0)/2 ...)
+        h0, h1 = planes[mg, c, tap, 0, q, lane, j], planes[mg, c, tap, 1, q, lane, j]
+        assert abs(h1) <= abs(h0) * 2.0 ** -8
+    assert np.array_equal(np.sort(total.reshape(-1)[total.reshape(-1) != 0]), np.sort(w.reshape(-1)[w.reshape(-1) != 0]).astype(np.float64))
+
+
 def test_lstm_pack_layout():
     lib = L.load()
     H = 32
@@ -78,7 +113,9 @@ def test_lstm_pack_layout():
 
 def test_bad_arguments_are_rejected_without_launching():
     lib = L.load()
-    assert lib.bc_conv1d_select_cfg(0, 4, 7, 1, 1) == -1
+    assert lib.bc_conv1d_select_cfg(0, 4, 7, 1, 1, 0) == -1
+    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 2) == -1  # unknown precision mode
+    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 1) in L.CONV_CFGS  # x6 needs Cin >= 16: fp32 kernel
     assert lib.bc_conv1d_packed_floats(8, 8, 0, 0) == -1
     assert lib.bc_conv1d_fwd(None, None, None, None, None, None, None, None, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4,
                              None) == 1

@@ -55,7 +55,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "x".join(map(str, c[:5])) + ("c" if c[5] else ""))
-def test_conv1d(dev, case):
+def test_conv1d(dev, case, prec):
     Cin, Cout, K, s, d, causal, use_snake, use_res, use_tanh, B, T = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     pad = 0 if causal else (K // 2 * d if s == 1 else s // 2 + s % 2)
@@ -102,7 +102,7 @@ CONVT_CASES = [
 
 
 @pytest.mark.parametrize("case", CONVT_CASES, ids=lambda c: "x".join(map(str, c[:3])) + ("c" if c[3] else ""))
-def test_conv_transpose1d(dev, case):
+def test_conv_transpose1d(dev, case, prec):
     Cin, Cout, s, causal, use_snake, B, T = case
     g = torch.Generator().manual_seed(7 + s)
     K = 2 * s if s != 1 else 1
@@ -163,7 +163,7 @@ def test_aa_activation(dev, golden):
 
 
 @pytest.mark.parametrize("H,layers,B,T", [(64, 2, 3, 50), (512, 1, 2, 20), (128, 2, 70, 9), (1536, 2, 2, 6)])
-def test_reslstm(dev, H, layers, B, T):
+def test_reslstm(dev, H, layers, B, T, prec):
     g = torch.Generator().manual_seed(H + T)
     m = BL.ResLSTM(H, num_layers=layers)
     with torch.no_grad():
@@ -179,6 +179,32 @@ def test_reslstm(dev, H, layers, B, T):
     got_s = m.run(x.to(dev), out_snake=snake.coeffs(dev)).cpu()
     want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
     assert_close_rel(got_s, want_s, 5e-5, f"lstm+snake H={H}")
+
+
+@pytest.mark.parametrize("Cin,Cout,K,d", [(384, 384, 7, 9), (1536, 1024, 3, 1), (96, 96, 7, 1), (768, 768, 1, 1)])
+def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
+    """The 3xbf16-split MFMA conv is fp32-accurate: its error against an fp64 evaluation is no larger
+    than (1.25x) the native fp32 MFMA kernel's, measured as max |y - y64| / max(sum |w x|)."""
+    g = torch.Generator().manual_seed(Cin + K)
+    m = CV.WNConv1d(Cin, Cout, kernel_size=K, dilation=d, padding=K // 2 * d)
+    conv = _rand_wn_conv(m, g)
+    x = torch.randn(2, Cin, 300, generator=g) * torch.exp(torch.randn(1, Cin, 1, generator=g))
+    sd = {k: v.detach() for k, v in conv.state_dict().items()}
+    w = O.wn_weight(sd, "").double()
+    y64 = F.conv1d(x.double(), w, sd["bias"].double(), 1, K // 2 * d, d)
+    scale = F.conv1d(x.double().abs(), w.abs(), None, 1, K // 2 * d, d).max()
+    m.to(dev)
+    errs = {}
+    old = L.precision_mode()
+    try:
+        for p in ("fp32", "x6"):
+            L.set_precision(p)
+            y = m.run(x.to(dev)).cpu().double()
+            errs[p] = float((y - y64).abs().max() / scale)
+    finally:
+        L._mode = old
+    assert errs["x6"] <= 1.25 * errs["fp32"] + 1e-9, errs
+    assert errs["fp32"] < 1e-6, errs
 
 
 def test_vq_argmin_bit_exact(dev, golden):

@@ -25,7 +25,7 @@ LAYER_FILES = sorted(f for f in os.listdir(GOLDEN) if f.startswith("layers_"))
 
 
 @pytest.mark.parametrize("fname", MODEL_FILES)
-def test_model_against_reference(dev, golden, fname):
+def test_model_against_reference(dev, golden, fname, prec):
     g = golden(fname)
     meta = g["meta"]
     enc, dec, _, _, ek, dk = build_models(meta["model"], device=dev, **meta["overrides"])
@@ -128,7 +128,7 @@ def test_full_size_batch_invariance_and_determinism(dev):
     assert len(torch.unique(c1)) > 50
 
 
-def test_full_size_clip_against_oracle(dev):
+def test_full_size_clip_against_oracle(dev, prec):
     """One full 10 s clip (default model) encoded on the GPU vs the CPU oracle; mismatches only at
     certified near-ties."""
     from audiotokenization_amd import synth
@@ -148,4 +148,4 @@ def test_full_size_clip_against_oracle(dev):
 
     gap = top2_gap(ze_ref, torch.from_numpy(dsd["quantizer.layers.0._codebook.weight"]))
     n_bad, worst = index_mismatches(codes.cpu().numpy(), codes_ref.numpy(), gap)
-    print(f"10 s default clip: {n_bad} / 1200 index mismatches, worst certified gap {worst:.2e}")
+    print(f"10 s default clip [{prec}]: {n_bad} / 1200 index mismatches, worst certified gap {worst:.2e}")
