@@ -30,8 +30,9 @@ _SIGS = {
     "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
     "bc_aa_snake_fwd": (I, [P, P, P, P, P, P, I, I, I, P]),
-    "bc_lstm_hh_packed_floats": (L, [I]),
-    "bc_lstm_pack_hh": (I, [P, P, I]),
+    "bc_lstm_hh_packed_floats": (L, [I, I]),
+    "bc_lstm_pack_hh": (I, [P, P, I, I]),
+    "bc_lstm_status": (I, [I]),
     "bc_lstm_workspace_floats": (L, [I, I, I]),
     "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
@@ -44,7 +45,7 @@ _SIGS = {
     "bc_synth_clips": (I, [P, I, L, L, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 2  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 3  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -168,7 +169,8 @@ CONV_CFGS = {t * 4 + b: _TILES[t] + (_BKC[b],) for t in range(5) for b in range(
 # csrc/conv1d_x6.hip kX6Tiles (cfg = 100 + index) -> (MT, NT, WM, WN)
 X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 4, 2), (2, 2, 4, 2), (6, 2, 1, 8),
                                               (4, 2, 1, 8), (3, 2, 1, 8), (2, 2, 1, 8), (1, 2, 1, 8), (6, 1, 1, 8),
-                                              (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8)])}
+                                              (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8),
+                                              (6, 2, 2, 4), (6, 1, 2, 4)])}
 
 
 def conv_kernel_name(cfg: int) -> str:

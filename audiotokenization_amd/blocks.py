@@ -199,8 +199,8 @@ class LSTM(nn.Module):
                 L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
                 wih.append(torch.from_numpy(packed).to(device))
                 w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
-                packed = np.empty(lib.bc_lstm_hh_packed_floats(H), dtype=np.float32)
-                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H)
+                packed = np.empty(lib.bc_lstm_hh_packed_floats(H, L.precision_mode()), dtype=np.float32)
+                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, L.precision_mode())
                 whh.append(torch.from_numpy(packed).to(device))
                 b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
                 bias.append(b.contiguous().to(device))

@@ -115,14 +115,21 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
                          S(stream));
 }
 
-long long bc_lstm_hh_packed_floats(int H) {
-  if (H <= 0 || H % 16) return -1;
+static bool lstm_use_seq(int H, int mode) { return mode == 1 && lstm_seq_ok(H); }
+
+long long bc_lstm_hh_packed_floats(int H, int mode) {
+  if (H <= 0 || H % 16 || (mode != 0 && mode != 1)) return -1;
+  if (lstm_use_seq(H, mode)) return lstm_seq_packed_bytes(H) / 4;
   return (long long)4 * H * H;
 }
 
-int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H) {
-  if (!w_hh_host || !packed_host || H <= 0 || H % 16) return BC_ERR_ARG;
-  if (lstm_fast_ok(H))
+int bc_lstm_status(int reset) { return lstm_seq_read_status(reset); }
+
+int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode) {
+  if (!w_hh_host || !packed_host || H <= 0 || H % 16 || (mode != 0 && mode != 1)) return BC_ERR_ARG;
+  if (lstm_use_seq(H, mode))
+    lstm_seq_pack(w_hh_host, reinterpret_cast<unsigned short*>(packed_host), H);  // persistent kernel
+  else if (lstm_fast_ok(H))
     lstm_pack_hh2(w_hh_host, packed_host, H);  // layout of the register-resident fast step kernel
   else
     lstm_pack_hh(w_hh_host, packed_host, H);
@@ -135,7 +142,9 @@ static long long lstm_frag_floats(int B, int H) { return (long long)((B + 63) / 
 long long bc_lstm_workspace_floats(int B, int H, int T) {
   if (B < 0 || H <= 0 || T < 0) return -1;
   const long long tb = (long long)T * B;
-  return tb * H * 3 + tb * 4 * H + (long long)H * B + 2 * lstm_frag_floats(B, H);
+  const long long frag = 2 * lstm_frag_floats(B, H);
+  const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
+  return tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq);
 }
 
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
@@ -173,6 +182,14 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
     a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
     rc = conv_launch(a, 1, cfg, st);
     if (rc) return rc;
+    if (lstm_use_seq(H, mode)) {
+      // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
+      rc = lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(w_hh_packed[l]), lout, cst, H, T, B, st);
+      if (rc) return rc;
+      lin = lout;
+      lout = (lout == ya) ? yb : ya;
+      continue;
+    }
     for (int t = 0; t < T; ++t) {
       rc = fast ? lstm_step_frag_launch(gx, w_hh_packed[l], frag[(t + 1) & 1], frag[t & 1], lout, cst,
                                         H, B, T, t, st)

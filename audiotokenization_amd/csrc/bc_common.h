@@ -61,6 +61,12 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// Workgroup barrier for LDS hand-offs that leaves outstanding global loads in flight: the compiler
+// drains vmcnt in front of __syncthreads(), which would also wait for prefetches meant to land
+// later.  LDS writes are drained (lgkmcnt), the "memory" clobber keeps the compiler from moving
+// memory accesses across it; LDS-DMA that must have landed is waited for explicitly (vmcnt).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // splitmix64 finalizer (SURVEY.md §8(d) synthetic input spec).

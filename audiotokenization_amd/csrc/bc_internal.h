@@ -18,6 +18,7 @@ struct ConvArgs {
   int yT, ostride, ooff;
   int epi;             // 0 none, 1 tanh
   // filled by conv_launch
+  int vec;             // 16-byte epilogue accesses allowed (conv_epilogue_vec_ok)
   int nchunks, win, bstage, astage;
   float inv_win;
   int ntm, ntn, nwg;
@@ -49,6 +50,13 @@ void lstm_pack_hh2(const float* w, float* out, int H);
 int lstm_step_frag_launch(const float* gx, const float* whh_p2, const float* hin, float* hout,
                           float* y, float* cst, int H, int B, int T, int t, hipStream_t st);
 void lstm_pack_hh(const float* w, float* out, int H);
+bool lstm_seq_ok(int H);
+long long lstm_seq_packed_bytes(int H);
+void lstm_seq_pack(const float* w, unsigned short* out, int H);
+long long lstm_seq_workspace_bytes(int H, int T);
+int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
+                    hipStream_t st);
+int lstm_seq_read_status(int reset);
 int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
                      int T, int t, hipStream_t st);
 

@@ -28,6 +28,7 @@
 // stride `s` (bc_convT1d_fwd in abi.hip).
 #include "bc_common.h"
 #include "bc_internal.h"
+#include "conv_epilogue.h"
 
 namespace bc {
 
@@ -126,47 +127,15 @@ __global__ void __launch_bounds__(256) conv1d_mfma_kernel(ConvArgs a) {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+          // operands swapped: the tile comes out transposed (positions x channels), see
+          // conv_epilogue.h
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[j], av[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // ---- epilogue: C/D map of 16x16x4: col = lane&15 (n), row = (lane>>4)*4 + r (m) ----------
-  float* yb = a.y + (long long)b * a.ybs;
-  float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
-  const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = m0 + wm * MT * 16 + i * 16 + (lane >> 4) * 4 + r;
-      if (co >= a.Cout) continue;
-      const float bias = a.bias ? a.bias[co] : 0.f;
-      const float sa = a.osa ? a.osa[co] : 0.f;
-      const float sb = a.osa ? a.osb[co] : 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + wn * NT * 16 + j * 16 + (lane & 15);
-        if (n >= a.Nout) continue;
-        const long long yi = (long long)co * a.yT + (long long)n * a.ostride + a.ooff;
-        float v = acc[i][j][r] + bias;
-        if (rb) v = rb[yi] + v;
-        if (a.epi == 1) v = tanhf(v);
-        if (a.osa) {
-          const float sv = snake(v, sa, sb);
-          if (y2b) {
-            yb[yi] = v;
-            y2b[yi] = sv;
-          } else {
-            yb[yi] = sv;
-          }
-        } else {
-          yb[yi] = v;
-        }
-      }
-    }
-  }
+  conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -330,6 +299,7 @@ static int launch_tile(ConvArgs& a, int B, hipStream_t st) {
   case T * 4 + 3: return launch_tile<MT, WM, NT, WN, 4>(a, B, st);
 
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st) {
+  a.vec = conv_epilogue_vec_ok(a);
   if (x6_cfg_valid(cfg_id)) return x6_launch(a, B, cfg_id, st);
   switch (cfg_id) {
     BC_TILE_CASES(0, 4, 2, 4, 2)

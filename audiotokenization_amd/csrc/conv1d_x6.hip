@@ -22,6 +22,7 @@
 
 #include "bc_common.h"
 #include "bc_internal.h"
+#include "conv_epilogue.h"
 
 namespace bc {
 
@@ -32,7 +33,8 @@ typedef __attribute__((address_space(3))) void* lds_void_t;
 
 constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
 constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
-constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352
+constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352 (22 B loads / thread)
+static_assert(2 * X6_MAXCOL_ITERS == 22, "the vmcnt(22) in the main loop counts the B loads");
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   const bf16x2_t v = __builtin_convertvector((float2_t){a, b}, bf16x2_t);
@@ -162,60 +164,34 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
         const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
+          // operands swapped (input as A): the tile comes out transposed, see conv_epilogue.h
           floatx4 t = acc[i][j];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[j][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][1], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][2], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][1], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][2], a0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
           acc[i][j] = t;
         }
       }
       if (tap == K - 1 && c + 1 < a.nchunks) {
-        __syncthreads();  // every wave is done reading this chunk's B tile
+        lds_barrier();  // every wave is done reading this chunk's B tile
         store_b();
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
+      // tap 0 of a multi-tap chunk the 2*X6_MAXCOL_ITERS B loads of the next chunk were issued
+      // after it and may stay in flight (vmcnt retires in issue order); they are consumed at the
+      // chunk's last tap, where the compiler waits for their registers itself.
+      if (tap == 0 && K > 1 && c + 1 < a.nchunks)
+        asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
     }
   }
 
-  // ---- epilogue (C/D layout of 16x16x32 == 16x16x4: col = lane&15, row = (lane>>4)*4 + r) -----
-  float* yb = a.y + (long long)b * a.ybs;
-  float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
-  const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = m0 + wm * MT * 16 + i * 16 + (lane >> 4) * 4 + r;
-      if (co >= a.Cout) continue;
-      const float bias = a.bias ? a.bias[co] : 0.f;
-      const float sa = a.osa ? a.osa[co] : 0.f;
-      const float sb = a.osa ? a.osb[co] : 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + wn * NT * 16 + j * 16 + (lane & 15);
-        if (n >= a.Nout) continue;
-        const long long yi = (long long)co * a.yT + (long long)n * a.ostride + a.ooff;
-        float v = acc[i][j][r] + bias;
-        if (rb) v = rb[yi] + v;
-        if (a.epi == 1) v = tanhf(v);
-        if (a.osa) {
-          const float sv = snake(v, sa, sb);
-          if (y2b) {
-            yb[yi] = v;
-            y2b[yi] = sv;
-          } else {
-            yb[yi] = sv;
-          }
-        } else {
-          yb[yi] = v;
-        }
-      }
-    }
-  }
+  conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -240,6 +216,8 @@ static const X6Tile kX6Tiles[] = {
     {3, 1, 1, 8},  // 111: BM=48  BN=128
     {2, 1, 1, 8},  // 112: BM=32  BN=128
     {1, 1, 1, 8},  // 113: BM=16  BN=128
+    {6, 2, 2, 4},  // 114: BM=192 BN=128  (Cout = 192k, stride <= 2)
+    {6, 1, 2, 4},  // 115: BM=192 BN=64
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -256,8 +234,13 @@ bool x6_cfg_valid(int cfg) { return cfg >= 100 && cfg < 100 + X6_NT; }
 // Returns a x6 cfg id, or -1 when the shape should stay on the fp32 kernel.
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
-  int order[4];
+  int order[6];
   int n = 0;
+  if (Cout >= 128 && Cout % 128 != 0 && Cout % 192 == 0) {
+    // 192-row tiles: no half-empty m-tile at C = 192 / 576
+    if (s <= 2) order[n++] = 14;
+    order[n++] = 15;
+  }
   if (Cout >= 128) {
     if (s == 1) order[n++] = 0;
     if (s <= 2) order[n++] = 1;
@@ -367,6 +350,8 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
     case 111: return launch_x6<3, 1, 1, 8>(a, B, st);
     case 112: return launch_x6<2, 1, 1, 8>(a, B, st);
     case 113: return launch_x6<1, 1, 1, 8>(a, B, st);
+    case 114: return launch_x6<6, 2, 2, 4>(a, B, st);
+    case 115: return launch_x6<6, 1, 2, 4>(a, B, st);
   }
   return BC_ERR_ARG;
 }

@@ -1,0 +1,96 @@
+// Shared epilogue of the conv kernels (conv1d.hip fp32 MFMA, conv1d_x6.hip 3xbf16 MFMA).
+//
+// Both kernels issue their MFMAs with the operands swapped (input fragment as "A", weight fragment
+// as "B"), which computes the TRANSPOSED output tile: in the 16x16 C/D layout a lane then holds
+// four CONSECUTIVE output positions of ONE output channel,
+//   co = tile_row0 + (lane & 15),   n = tile_col0 + (lane >> 4) * 4 + r   (r = 0..3),
+// so the epilogue reads the residual and writes the outputs as one 16-byte access per lane and
+// tile (4x fewer store instructions than a channel-per-register layout, the store-issue bound of a
+// k=1 conv's epilogue), and fetches bias / Snake coefficients once per channel.
+// Op order per element is the reference's: (acc + bias), residual + that, then tanh or Snake.
+#pragma once
+#include "bc_common.h"
+#include "bc_internal.h"
+
+namespace bc {
+
+__device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, float bias, float res,
+                                                bool has_res) {
+  float v = acc + bias;
+  if (has_res) v = res + v;
+  if (a.epi == 1) v = tanhf(v);
+  return v;
+}
+
+// acc[i][j]: transposed 16x16 tiles; rows (channels) start at row0 + 16 i, columns (positions) at
+// col0 + 16 j.
+template <int MT, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
+                                              int col0, int lane) {
+  float* yb = a.y + (long long)b * a.ybs;
+  float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
+  const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
+  const bool snk = a.osa != nullptr;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int co = row0 + i * 16 + (lane & 15);
+    if (co >= a.Cout) continue;
+    const float bias = a.bias ? a.bias[co] : 0.f;
+    const float sa = snk ? a.osa[co] : 0.f;
+    const float sb = snk ? a.osb[co] : 0.f;
+    const long long rowoff = (long long)co * a.yT + a.ooff;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int nb = col0 + j * 16 + (lane >> 4) * 4;
+      if (nb >= a.Nout) continue;
+      if (a.vec && nb + 3 < a.Nout) {
+        const long long yi = rowoff + nb;
+        floatx4 r = {0.f, 0.f, 0.f, 0.f};
+        if (rb) r = *reinterpret_cast<const floatx4*>(rb + yi);
+        floatx4 v, sv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = conv_epi_value(a, acc[i][j][q], bias, r[q], rb != nullptr);
+          sv[q] = snk ? snake(v[q], sa, sb) : v[q];
+        }
+        if (y2b) {
+          *reinterpret_cast<floatx4*>(yb + yi) = v;
+          *reinterpret_cast<floatx4*>(y2b + yi) = sv;
+        } else {
+          *reinterpret_cast<floatx4*>(yb + yi) = sv;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = nb + q;
+          if (n >= a.Nout) break;
+          const long long yi = rowoff + (long long)n * a.ostride;
+          const float v = conv_epi_value(a, acc[i][j][q], bias, rb ? rb[yi] : 0.f, rb != nullptr);
+          if (snk) {
+            const float sv = snake(v, sa, sb);
+            if (y2b) {
+              yb[yi] = v;
+              y2b[yi] = sv;
+            } else {
+              yb[yi] = sv;
+            }
+          } else {
+            yb[yi] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Host: may the epilogue use 16-byte accesses for this launch?  (unit output stride, every row
+// and batch offset a multiple of 4 floats, 16-byte aligned base pointers)
+inline int conv_epilogue_vec_ok(const ConvArgs& a) {
+  auto al = [](const void* p) { return ((unsigned long long)p & 15ull) == 0; };
+  if (a.ostride != 1 || a.yT % 4 || a.ooff % 4 || a.ybs % 4) return 0;
+  if (!al(a.y) || (a.y2 && !al(a.y2))) return 0;
+  if (a.res && (a.rbs % 4 || !al(a.res))) return 0;
+  return 1;
+}
+
+}  // namespace bc

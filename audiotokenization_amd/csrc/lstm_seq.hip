@@ -1,0 +1,400 @@
+// Persistent ResLSTM recurrence (vq/module.py:143-167 -> torch.nn.LSTM, batch_first,
+// unidirectional): ONE launch per layer walks all T steps.
+//
+// Why persistent: one step of the default model (H = 1536, 64 clips) is a 6144 x 1536 x 64 GEMM
+// plus the cell update.  As one launch per step (lstm.hip) every step re-reads W_hh (37.7 MB) from
+// the Infinity Cache and pays a kernel boundary.  Here every workgroup keeps its slice of W_hh in
+// VGPRs for the whole sequence; the only per-step traffic is h_{t-1} (H x 64 fp32, read by every
+// workgroup from L2) and a per-workgroup flag.
+//
+// Geometry: G = H / 8 workgroups (192 for H = 1536, one per CU, all co-resident), 256 threads.
+//   workgroup g owns hidden units 8g..8g+7 = 32 gate rows = two 16-row m-tiles whose rows are
+//   unit-major (m = 4*unit + gate), so after the MFMA a lane holds the i,f,g,o pre-activations of
+//   one (unit, clip) cell in its four accumulator registers.
+//   wave w owns K = [w*H/4, (w+1)*H/4): KS = H/128 k-steps of 32; its W_hh fragments (2 m-tiles x
+//   KS x 3 bf16 planes) are loaded once.
+// Arithmetic: the fp32-accurate 3xbf16 split of conv1d_x6.hip (six bf16 MFMAs per product term);
+//   h is split on the fly, W_hh on the host.  The four waves' partial sums are reduced through LDS
+//   in a fixed order, then c = f*c + i*g, h = o*tanh(c) with c held in registers.
+// Hand-off of h_t: the workgroup gathers its 8 units x 64 clips in LDS, one wave writes them with
+//   16-byte write-through (sc1) stores into slot t of the fragment-native sequence buffer
+//   hseq[t][k-step][n-tile][lane][8], drains them (vmcnt(0)) and one lane stores flags[g] = t+1
+//   (relaxed, agent scope).  Consumer wave w polls the flags of the G/4 workgroups that produce its
+//   K range (sc1 loads, bounded spin), then reads slot t-1 with PLAIN loads: every slot is written
+//   once per launch and read only after its flag, so no L1/L2 of this launch can hold an older
+//   copy of those lines (kernel boundaries invalidate the caches), and the first CU of an XCD to
+//   miss pulls the line into that XCD's L2 for the other 23.  (Measured: sc1 loads of a reused
+//   double buffer instead — every CU fetching its 393 KB over the fabric — cost 11.6 us per step.)
+//   Every poll is bounded: on timeout the kernel counts it in *status and all workgroups leave.
+#include <cstring>
+
+#include "bc_common.h"
+#include "bc_internal.h"
+
+namespace bc {
+
+typedef __bf16 ls_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 ls_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float ls_float2 __attribute__((ext_vector_type(2)));
+typedef unsigned ls_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned ls_gu32;
+
+constexpr int LS_U = 8;          // hidden units per workgroup
+constexpr int LS_WAVES = 4;
+constexpr int LS_NB = 64;        // clips per launch (4 n-tiles of 16)
+constexpr int LS_SC1 = 16;       // buffer-op cache policy: sc1 (write-through / L1 bypass)
+constexpr unsigned LS_SPIN_LIMIT = 1u << 22;
+
+struct LstmSeqArgs {
+  const float* gx;            // [4H][T*Btot] input projection incl. b_ih + b_hh (ctb layout)
+  const unsigned short* whh;  // lstm_seq_pack layout
+  float* y;                   // [H][T*Btot] output h_t (ctb layout)
+  float* hseq;                // [T][H/32][4][64][8] fp32: h_t in MFMA-fragment order, one slot per step
+  unsigned* flags;            // [G], zero before the launch
+  int* status;                // timeout counter (0 = ok)
+  int H, T, Btot, b0, nb;
+  int dbg;  // timing experiments only (BC_LSTM_SEQ_DEBUG): 4 = skip the flag poll (wrong results)
+};
+
+__device__ __forceinline__ unsigned ls_pk(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((ls_float2){a, b}, ls_bf16x2));
+}
+
+// split 8 fp32 values into three bf16x8 planes, v = p0 + p1 + p2 exactly
+__device__ __forceinline__ void ls_split8(const float (&v)[8], ls_bf16x8 (&p)[3]) {
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = v[2 * i], b = v[2 * i + 1];
+    h[i] = ls_pk(a, b);
+    const float ra = a - __uint_as_float(h[i] << 16), rb = b - __uint_as_float(h[i] & 0xffff0000u);
+    m[i] = ls_pk(ra, rb);
+    const float sa = ra - __uint_as_float(m[i] << 16), sb = rb - __uint_as_float(m[i] & 0xffff0000u);
+    l[i] = ls_pk(sa, sb);
+  }
+  p[0] = __builtin_bit_cast(ls_bf16x8, (ls_u32x4){h[0], h[1], h[2], h[3]});
+  p[1] = __builtin_bit_cast(ls_bf16x8, (ls_u32x4){m[0], m[1], m[2], m[3]});
+  p[2] = __builtin_bit_cast(ls_bf16x8, (ls_u32x4){l[0], l[1], l[2], l[3]});
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ls_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <int KS>
+__global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
+  __shared__ floatx4 red[LS_WAVES][8][64];  // per-wave partial gates of the 8 (m-tile, n-tile) tiles
+  __shared__ float hs[LS_NB][LS_U + 1];     // h_t gathered per clip
+  __shared__ int bail;
+
+  const int g = blockIdx.x;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H;
+  const long long TB = (long long)a.T * a.Btot;
+  if (tid == 0) bail = 0;
+
+  // ---- W_hh slice -> registers (once) ----
+  ls_bf16x8 wr[2][KS][3];
+  {
+    const ls_bf16x8* wp = reinterpret_cast<const ls_bf16x8*>(a.whh) + (long long)(g * LS_WAVES + w) * (2 * KS * 3) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wr[mt][ks][p] = wp[((mt * KS + ks) * 3 + p) * 64];
+  }
+
+  // cells of this thread: tiles p = 2w + q (q = 0, 1); m-tile p>>2, n-tile p&3
+  int cu[2], cb[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = 2 * w + q;
+    cu[q] = (p >> 2) * 4 + (lane >> 4);  // unit within the workgroup
+    cb[q] = (p & 3) * 16 + (lane & 15);  // clip within the launch
+  }
+  float cst[2] = {0.f, 0.f};
+
+  const long long hstep = (long long)H * LS_NB;  // floats of h per step in hseq
+  const int nprod = G / LS_WAVES;                // producers of this wave's K range
+  ls_gu32* flags = (ls_gu32*)(a.flags);
+
+  // input-projection gates of my two cells (independent of the recurrence: prefetched a step ahead)
+  auto load_gx = [&](int t, float (&dst)[2][4]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int unit = g * LS_U + cu[q];
+      const bool ok = cb[q] < a.nb;
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate)
+        dst[q][gate] = ok ? a.gx[((long long)gate * H + unit) * TB + (long long)t * a.Btot + a.b0 + cb[q]] : 0.f;
+    }
+  };
+  float gxv[2][4], gxn[2][4];
+  load_gx(0, gxv);
+
+  for (int t = 0; t < a.T; ++t) {
+
+    floatx4 acc[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if (t > 0) {
+      // wait until the producers of h_{t-1}[my K range] have published step t-1
+      const int p0 = w * nprod;
+      unsigned spins = 0;
+      while (!(a.dbg & 4)) {
+        const unsigned f = lane < nprod ? __hip_atomic_load(flags + p0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0xffffffffu;
+        if (__all(f >= (unsigned)t)) break;
+        if (++spins > LS_SPIN_LIMIT) {
+          if (lane == 0) {
+            atomicAdd(a.status, 1);
+            bail = 1;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
+      // h_{t-1} lives at addresses no cache of this launch has seen before it was written through
+      // (one slot per step), so plain L2-cached loads are fresh and the XCD's L2 serves its CUs.
+      // Register double buffer: the 8 loads of k-step ks+1 are in flight while k-step ks runs its
+      // 48 MFMAs (one wave per SIMD: nothing else hides the L2 latency).
+      const floatx4* hp = reinterpret_cast<const floatx4*>(a.hseq + (long long)(t - 1) * hstep) + lane * 2;
+      floatx4 hbuf[2][4][2];
+      auto load_ks = [&](int ks, floatx4 (&dst)[4][2]) {
+        const int ksa = w * KS + ks;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          dst[nt][0] = hp[(ksa * 4 + nt) * 128];
+          dst[nt][1] = hp[(ksa * 4 + nt) * 128 + 1];
+        }
+      };
+      load_ks(0, hbuf[0]);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) load_ks(ks + 1, hbuf[(ks + 1) & 1]);
+        // keep the scheduler from sinking those loads to their uses (it does under this register
+        // pressure, serialising 96 L2 round trips per step)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          float hv[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            hv[i] = hbuf[ks & 1][nt][0][i];
+            hv[4 + i] = hbuf[ks & 1][nt][1][i];
+          }
+          ls_bf16x8 hb[3];
+          ls_split8(hv, hb);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            floatx4 s = acc[mt][nt];
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][2], hb[0], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][1], hb[1], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[2], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][1], hb[0], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[1], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[0], s, 0, 0, 0);
+            acc[mt][nt] = s;
+          }
+        }
+      }
+    }
+
+    // ---- reduce the four waves' partial sums (fixed order), cell update ----
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) red[w][mt * 4 + nt][lane] = acc[mt][nt];
+    __syncthreads();
+    if (bail) return;  // uniform: every wave reads it after the same barrier
+    float hq[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = 2 * w + q;
+      floatx4 hsum = red[0][p][lane];
+#pragma unroll
+      for (int ww = 1; ww < LS_WAVES; ++ww) {
+        const floatx4 r = red[ww][p][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hsum[i] = hsum[i] + r[i];
+      }
+      float gt[4];
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate) gt[gate] = t > 0 ? gxv[q][gate] + hsum[gate] : gxv[q][gate];
+      const float ig = sigmoidf_ref(gt[0]);
+      const float fg = sigmoidf_ref(gt[1]);
+      const float gg = tanhf(gt[2]);
+      const float og = sigmoidf_ref(gt[3]);
+      const float c = fg * cst[q] + ig * gg;
+      cst[q] = c;
+      hq[q] = cb[q] < a.nb ? og * tanhf(c) : 0.f;
+      hs[cb[q]][cu[q]] = hq[q];
+    }
+    __syncthreads();
+
+    // ---- publish h_t: wave 0, one clip per lane, 32 B write-through, drained, then the flag ----
+    if (w == 0 && t + 1 < a.T) {
+      const int b = lane, nt = b >> 4, c16 = b & 15;
+      const int ksa = g >> 2, qq = g & 3;
+      const __amdgpu_buffer_rsrc_t hr = ls_rsrc(a.hseq + (long long)t * hstep, (unsigned)(hstep * 4));
+      const unsigned off = (unsigned)(((ksa * 4 + nt) * 64 + qq * 16 + c16) * 32);
+      ls_u32x4 v0, v1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v0[i] = __float_as_uint(hs[b][i]);
+        v1[i] = __float_as_uint(hs[b][4 + i]);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, v0), hr, off, 0, LS_SC1);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, v1), hr, off + 16, 0, LS_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(flags + g, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // layer output (read only after the launch): off the publishing wave's critical path
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (cb[q] < a.nb) a.y[(long long)(g * LS_U + cu[q]) * TB + (long long)t * a.Btot + a.b0 + cb[q]] = hq[q];
+    // next step's input-projection gates: issued after this step's publish drain so that drain does
+    // not wait for them; they land during the next step's poll and MFMAs
+    if (t + 1 < a.T) {
+      load_gx(t + 1, gxn);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int gate = 0; gate < 4; ++gate) gxv[q][gate] = gxn[q][gate];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+bool lstm_seq_ok(int H) {
+  if (H % 128) return false;
+  const int ks = H / 128;
+  return ks == 2 || ks == 4 || ks == 8 || ks == 12;
+}
+
+long long lstm_seq_packed_bytes(int H) { return (long long)4 * H * H * 3 * 2; }
+
+static inline unsigned short ls_f2bf(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
+  return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+static inline float ls_bf2f(unsigned short h) {
+  const unsigned u = (unsigned)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// w: torch weight_hh [4H][H] (rows i, f, g, o).  out: [g][wave][mt][ks][plane][lane][8] bf16
+void lstm_seq_pack(const float* w, unsigned short* out, int H) {
+  const int KS = H / 128, G = H / LS_U;
+  long long o = 0;
+  for (int g = 0; g < G; ++g)
+    for (int wv = 0; wv < LS_WAVES; ++wv)
+      for (int mt = 0; mt < 2; ++mt)
+        for (int ks = 0; ks < KS; ++ks)
+          for (int p = 0; p < 3; ++p)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int j = 0; j < 8; ++j, ++o) {
+                const int m = lane & 15;
+                const int unit = g * LS_U + mt * 4 + (m >> 2);
+                const int row = (m & 3) * H + unit;
+                const int k = (wv * KS + ks) * 32 + 8 * (lane >> 4) + j;
+                const float v = w[(long long)row * H + k];
+                const unsigned short h0 = ls_f2bf(v);
+                const float r1 = v - ls_bf2f(h0);
+                const unsigned short h1 = ls_f2bf(r1);
+                const unsigned short h2 = ls_f2bf(r1 - ls_bf2f(h1));
+                out[o] = p == 0 ? h0 : p == 1 ? h1 : h2;
+              }
+}
+
+long long lstm_seq_workspace_bytes(int H, int T) {
+  return 1024 + (long long)T * H * LS_NB * 4;  // flags (<= 256 words) | hseq
+}
+
+__device__ int bc_lstm_seq_timeouts;  // bumped by a workgroup that gave up waiting (never in a good run)
+
+static int* status_word() {
+  static int* p = [] {
+    void* q = nullptr;
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(bc_lstm_seq_timeouts)) != hipSuccess) return (int*)nullptr;
+    return reinterpret_cast<int*>(q);
+  }();
+  return p;
+}
+
+int lstm_seq_read_status(int reset) {
+  int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(bc_lstm_seq_timeouts), sizeof(int)) != hipSuccess) return -1;
+  if (reset) {
+    const int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(bc_lstm_seq_timeouts), &z, sizeof(int)) != hipSuccess) return -1;
+  }
+  return v;
+}
+
+static int device_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return v;
+  }();
+  return n;
+}
+
+int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
+                    hipStream_t st) {
+  if (!lstm_seq_ok(H)) return BC_ERR_UNSUPPORTED;
+  const int G = H / LS_U;
+  if (G > 256 || G > device_cus()) return BC_ERR_UNSUPPORTED;  // every workgroup must be resident
+  int* status = status_word();
+  if (!status) return BC_ERR_LAUNCH;
+  LstmSeqArgs a{};
+  a.gx = gx;
+  a.whh = whh;
+  a.y = y;
+  a.flags = reinterpret_cast<unsigned*>(ws);
+  a.hseq = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + 1024);
+  a.status = status;
+  a.H = H;
+  a.T = T;
+  a.Btot = Btot;
+  static const int dbg = [] {
+    const char* e = getenv("BC_LSTM_SEQ_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
+  for (int b0 = 0; b0 < Btot; b0 += LS_NB) {
+    a.b0 = b0;
+    a.nb = Btot - b0 < LS_NB ? Btot - b0 : LS_NB;
+    if (hipMemsetAsync(a.flags, 0, 1024, st) != hipSuccess) return BC_ERR_LAUNCH;
+    switch (H / 128) {
+      case 2: hipLaunchKernelGGL(lstm_seq_x6_kernel<2>, dim3(G), dim3(256), 0, st, a); break;
+      case 4: hipLaunchKernelGGL(lstm_seq_x6_kernel<4>, dim3(G), dim3(256), 0, st, a); break;
+      case 8: hipLaunchKernelGGL(lstm_seq_x6_kernel<8>, dim3(G), dim3(256), 0, st, a); break;
+      case 12: hipLaunchKernelGGL(lstm_seq_x6_kernel<12>, dim3(G), dim3(256), 0, st, a); break;
+      default: return BC_ERR_UNSUPPORTED;
+    }
+    BC_CHECK_LAUNCH();
+  }
+  return BC_OK;
+}
+
+}  // namespace bc

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 2
+#define BC_ABI_VERSION 3
 
 int bc_abi_version(void);
 
@@ -87,13 +87,18 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
  * num_layers, batch_first=True) (unidirectional), + skip, rearrange back.  x, out: [B][H][T].
  * Per layer l: w_ih_packed[l] = bc_conv1d_pack(weight_ih_l{l} as [4H][H][1], cfg =
  * bc_conv1d_select_cfg(4H, H, 1, 1, 1, mode)); bias[l] = bias_ih_l{l} + bias_hh_l{l} ([4H], device);
- * w_hh_packed[l] = bc_lstm_pack_hh(weight_hh_l{l}).  The three pointer arrays are HOST arrays of
- * device pointers.  out = snake(y + x) when out_snake_alpha_exp != NULL (the Activation1d that
- * follows the ResLSTM in both stacks), else y + x.  workspace: bc_lstm_workspace_floats(B, H, T)
- * device floats.  H % 16 == 0. */
-long long bc_lstm_hh_packed_floats(int H);
-int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H);
+ * w_hh_packed[l] = bc_lstm_pack_hh(weight_hh_l{l}, mode) (same mode as the forward call).  The three
+ * pointer arrays are HOST arrays of device pointers.  out = snake(y + x) when out_snake_alpha_exp !=
+ * NULL (the Activation1d that follows the ResLSTM in both stacks), else y + x.  workspace:
+ * bc_lstm_workspace_floats(B, H, T) device floats.  H % 16 == 0.
+ * mode 1 with H in {256, 512, 1024, 1536}: the recurrence runs as ONE persistent launch per layer
+ * (H/8 co-resident workgroups, W_hh register-resident, 3xbf16-split MFMA); otherwise one launch per
+ * step (fp32 MFMA).  bc_lstm_status(reset) returns how many persistent-launch workgroups gave up
+ * waiting for a neighbour (bounded spin; 0 in every correct run), synchronising the device. */
+long long bc_lstm_hh_packed_floats(int H, int mode);
+int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode);
 long long bc_lstm_workspace_floats(int B, int H, int T);
+int bc_lstm_status(int reset);
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,

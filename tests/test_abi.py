@@ -102,13 +102,37 @@ def test_lstm_pack_layout():
     lib = L.load()
     H = 32
     w = np.arange(4 * H * H, dtype=np.float32).reshape(4 * H, H)
-    out = np.empty(lib.bc_lstm_hh_packed_floats(H), np.float32)
-    assert lib.bc_lstm_pack_hh(w.ctypes.data, out.ctypes.data, H) == 0
-    P = out.reshape(H // 4, H // 4, 64)
-    for ug, ks, lane in [(0, 0, 0), (3, 5, 17), (7, 7, 63)]:
+    for mode in (0, 1):  # H = 32: no persistent x6 kernel, both modes use the per-step layout
+        out = np.empty(lib.bc_lstm_hh_packed_floats(H, mode), np.float32)
+        assert lib.bc_lstm_pack_hh(w.ctypes.data, out.ctypes.data, H, mode) == 0
+        P = out.reshape(H // 4, H // 4, 64)
+        for ug, ks, lane in [(0, 0, 0), (3, 5, 17), (7, 7, 63)]:
+            m = lane & 15
+            assert P[ug, ks, lane] == w[(m >> 2) * H + ug * 4 + (m & 3), ks * 4 + (lane >> 4)]
+        assert sorted(out.tolist()) == sorted(w.reshape(-1).tolist())
+
+
+@pytest.mark.parametrize("H", [256, 512])
+def test_lstm_seq_pack_layout(H):
+    """mode 1: W_hh as three exact bf16 planes in the persistent kernel's register order
+    [workgroup][wave][m-tile][k-step][plane][lane][8], m-tile rows unit-major (m = 4*unit + gate)."""
+    lib = L.load()
+    rng = np.random.default_rng(H)
+    w = (rng.standard_normal((4 * H, H)) / np.sqrt(H)).astype(np.float32)
+    n = lib.bc_lstm_hh_packed_floats(H, 1)
+    assert n * 4 == 4 * H * H * 3 * 2
+    out = np.empty(n, np.float32)
+    assert lib.bc_lstm_pack_hh(w.ctypes.data, out.ctypes.data, H, 1) == 0
+    KS, G = H // 128, H // 8
+    planes = _bf16_to_f64(out.view(np.uint16).reshape(G, 4, 2, KS, 3, 64, 8))
+    total = planes.sum(axis=4)
+    for _ in range(300):
+        g, wv, mt, ks, lane, j = (rng.integers(s) for s in total.shape)
         m = lane & 15
-        assert P[ug, ks, lane] == w[(m >> 2) * H + ug * 4 + (m & 3), ks * 4 + (lane >> 4)]
-    assert sorted(out.tolist()) == sorted(w.reshape(-1).tolist())
+        row = (m & 3) * H + g * 8 + mt * 4 + (m >> 2)
+        k = (wv * KS + ks) * 32 + 8 * (lane >> 4) + j
+        assert total[g, wv, mt, ks, lane, j] == float(w[row, k])
+    assert np.array_equal(np.sort(total.reshape(-1)), np.sort(w.reshape(-1).astype(np.float64)))
 
 
 def test_bad_arguments_are_rejected_without_launching():
@@ -121,7 +145,8 @@ def test_bad_arguments_are_rejected_without_launching():
                              None) == 1
     # dual output without an epilogue Snake, tanh together with a Snake: rejected
     assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, 1, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4, None) == 1
-    assert lib.bc_lstm_hh_packed_floats(10) == -1
+    assert lib.bc_lstm_hh_packed_floats(10, 0) == -1
+    assert lib.bc_lstm_hh_packed_floats(512, 3) == -1
     assert lib.bc_vq_prepare_codebook(1, 1, 1, 8192, 16, None) == 3
     assert lib.bc_synth_clips(None, 1, 10, 0, None) == 1
     assert lib.bc_convT1d_phase_taps(10, 5) == 2 and lib.bc_convT1d_phase_taps(1, 1) == 1

@@ -162,8 +162,11 @@ def test_aa_activation(dev, golden):
         assert_close_rel(got, torch.from_numpy(gd[f"y_{T}"]), 2e-6, f"aa T={T}")
 
 
-@pytest.mark.parametrize("H,layers,B,T", [(64, 2, 3, 50), (512, 1, 2, 20), (128, 2, 70, 9), (1536, 2, 2, 6)])
+@pytest.mark.parametrize("H,layers,B,T", [(64, 2, 3, 50), (512, 1, 2, 20), (128, 2, 70, 9), (1536, 2, 2, 6),
+                                          (256, 2, 130, 7), (512, 2, 64, 40), (1536, 1, 64, 25)])
 def test_reslstm(dev, H, layers, B, T, prec):
+    """x6 mode with H in {256, 512, 1024, 1536} runs the persistent kernel (lstm_seq.hip), including
+    batch slicing (B = 130 -> 3 launches per layer); bc_lstm_status must report no timed-out wait."""
     g = torch.Generator().manual_seed(H + T)
     m = BL.ResLSTM(H, num_layers=layers)
     with torch.no_grad():
@@ -179,6 +182,7 @@ def test_reslstm(dev, H, layers, B, T, prec):
     got_s = m.run(x.to(dev), out_snake=snake.coeffs(dev)).cpu()
     want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
     assert_close_rel(got_s, want_s, 5e-5, f"lstm+snake H={H}")
+    assert L.load().bc_lstm_status(1) == 0
 
 
 @pytest.mark.parametrize("Cin,Cout,K,d", [(384, 384, 7, 9), (1536, 1024, 3, 1), (96, 96, 7, 1), (768, 768, 1, 1)])
