@@ -174,16 +174,18 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
 
 
 def conv_kernel_name(cfg: int) -> str:
-    if cfg in X6_CFGS:
-        mt, nt, wm, wn = X6_CFGS[cfg]
-        return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}>"
+    if cfg in X6_CFGS or cfg - 100 in X6_CFGS:
+        planes = 3 if cfg in X6_CFGS else 1
+        mt, nt, wm, wn = X6_CFGS[cfg if planes == 3 else cfg - 100]
+        return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
 
 
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6",
-# the default: same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling).
-PRECISIONS = {"fp32": 0, "x6": 1}
+# the default: same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
+# 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the LSTM stays fp32-accurate).
+PRECISIONS = {"fp32": 0, "x6": 1, "bf16": 2}
 _mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "x6")]
 
 
@@ -197,6 +199,11 @@ def set_precision(name: str) -> None:
 
 def precision_mode() -> int:
     return _mode
+
+
+def lstm_mode() -> int:
+    """Mode the ResLSTM packs and runs with (bc_reslstm_fwd maps bf16 to x6)."""
+    return 1 if _mode == 2 else _mode
 
 
 def precision_name() -> str:

@@ -191,7 +191,8 @@ class LSTM(nn.Module):
             H = self.hidden_size
             if self.input_size != H:
                 raise NotImplementedError("ResLSTM requires input_size == hidden_size")
-            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1, L.precision_mode())
+            mode = L.lstm_mode()
+            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1, mode)
             wih, whh, bias = [], [], []
             for l in range(self.num_layers):
                 w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
@@ -199,15 +200,15 @@ class LSTM(nn.Module):
                 L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
                 wih.append(torch.from_numpy(packed).to(device))
                 w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
-                packed = np.empty(lib.bc_lstm_hh_packed_floats(H, L.precision_mode()), dtype=np.float32)
-                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, L.precision_mode())
+                packed = np.empty(lib.bc_lstm_hh_packed_floats(H, mode), dtype=np.float32)
+                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, mode)
                 whh.append(torch.from_numpy(packed).to(device))
                 b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
                 bias.append(b.contiguous().to(device))
             arrs = (L.ptr_array([t.data_ptr() for t in wih]), L.ptr_array([t.data_ptr() for t in bias]),
                     L.ptr_array([t.data_ptr() for t in whh]))
             return (wih, whh, bias), arrs
-        return self._cache.get(_pkey(*self._plist()) + (str(device), L.precision_mode()), build)
+        return self._cache.get(_pkey(*self._plist()) + (str(device), L.lstm_mode()), build)
 
 
 class ResLSTM(nn.Module):

@@ -13,13 +13,15 @@ int bc_abi_version(void) { return BC_ABI_VERSION; }
 
 int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode) {
   if (Cout <= 0 || Cin <= 0 || K <= 0 || stride <= 0 || dilation <= 0) return -1;
-  if (mode != 0 && mode != 1) return -1;
+  if (mode < 0 || mode > 2) return -1;
   return conv_select_cfg(Cout, Cin, K, stride, dilation, mode);
 }
 
-// a cfg is acceptable for a shape if either precision mode selects it
+// a cfg is acceptable for a shape if some precision mode selects it
 static bool cfg_matches(int cfg, int Cout, int Cin, int K, int s, int d) {
-  return cfg == conv_select_cfg(Cout, Cin, K, s, d, 0) || cfg == conv_select_cfg(Cout, Cin, K, s, d, 1);
+  for (int m = 0; m <= 2; ++m)
+    if (cfg == conv_select_cfg(Cout, Cin, K, s, d, m)) return true;
+  return false;
 }
 
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg) {
@@ -115,10 +117,12 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
                          S(stream));
 }
 
-static bool lstm_use_seq(int H, int mode) { return mode == 1 && lstm_seq_ok(H); }
+// The recurrence is accuracy-critical: mode 2 (bf16 conv products) keeps the LSTM fp32-accurate.
+static int lstm_mode(int mode) { return mode == 2 ? 1 : mode; }
+static bool lstm_use_seq(int H, int mode) { return lstm_mode(mode) == 1 && lstm_seq_ok(H); }
 
 long long bc_lstm_hh_packed_floats(int H, int mode) {
-  if (H <= 0 || H % 16 || (mode != 0 && mode != 1)) return -1;
+  if (H <= 0 || H % 16 || mode < 0 || mode > 2) return -1;
   if (lstm_use_seq(H, mode)) return lstm_seq_packed_bytes(H) / 4;
   return (long long)4 * H * H;
 }
@@ -126,7 +130,7 @@ long long bc_lstm_hh_packed_floats(int H, int mode) {
 int bc_lstm_status(int reset) { return lstm_seq_read_status(reset); }
 
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode) {
-  if (!w_hh_host || !packed_host || H <= 0 || H % 16 || (mode != 0 && mode != 1)) return BC_ERR_ARG;
+  if (!w_hh_host || !packed_host || H <= 0 || H % 16 || mode < 0 || mode > 2) return BC_ERR_ARG;
   if (lstm_use_seq(H, mode))
     lstm_seq_pack(w_hh_host, reinterpret_cast<unsigned short*>(packed_host), H);  // persistent kernel
   else if (lstm_fast_ok(H))
@@ -152,10 +156,11 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
                    const float* out_snake_inv_beta, float* workspace, int mode, void* stream) {
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
-      H % 16 || T < 0 || num_layers <= 0 || (mode != 0 && mode != 1))
+      H % 16 || T < 0 || num_layers <= 0 || mode < 0 || mode > 2)
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
+  mode = lstm_mode(mode);
   hipStream_t st = S(stream);
   const long long tb = (long long)T * B;
   if (tb > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;

@@ -24,10 +24,10 @@ struct ConvArgs {
   int ntm, ntn, nwg;
 };
 // mode 0: fp32 MFMA kernel (cfg 0..19); mode 1: fp32-accurate 3xbf16 kernel (cfg 100..) where the
-// shape suits it, else the fp32 kernel.
+// shape suits it, else the fp32 kernel; mode 2: plain bf16 products (cfg 200..), else fp32.
 int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode = 0);
 bool conv_cfg_valid(int cfg_id);
-int x6_select_cfg(int Cout, int Cin, int K, int s, int d);
+int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes);
 bool x6_cfg_valid(int cfg);
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg);
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg);

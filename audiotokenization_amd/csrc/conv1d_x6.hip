@@ -43,7 +43,9 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
 __device__ __forceinline__ float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
 
-template <int MT, int NT, int WM, int WN>
+// P = operand planes: 3 (x6, fp32-accurate) or 1 (plain bf16 products: the "bf16" precision mode of
+// BASELINE config 5, activations still stored fp32).
+template <int MT, int NT, int WM, int WN, int P>
 __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
@@ -53,7 +55,7 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
   const int ncol = a.win;                // columns of the input tile
   const int bplane = a.bstage;           // bytes per B plane (multiple of 16)
   unsigned char* Bs = smem_x6;                            // [3][ncol][80 B]
-  unsigned char* As = smem_x6 + 3 * bplane;               // [2][3][QA][1 KiB]
+  unsigned char* As = smem_x6 + P * bplane;               // [2][P][QA][1 KiB]
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int mt_idx = wg % a.ntm;
@@ -79,7 +81,7 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
 
   const int K = a.K;
   const int nsteps = a.nchunks * K;
-  const int a_pieces = 3 * QA;
+  const int a_pieces = P * QA;
   const unsigned char* wblk = reinterpret_cast<const unsigned char*>(a.w) +
                               (long long)mt_idx * a.nchunks * K * (a_pieces * 1024);
 
@@ -115,14 +117,16 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
       if (col < ncol) {
         const float v0 = bv0[i], v1 = bv1[i];
         const unsigned h = pk_bf16(v0, v1);
-        const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
-        const unsigned m = pk_bf16(r0, r1);
-        const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
-        const unsigned l = pk_bf16(s0, s1);
         unsigned char* p = Bs + col * X6_PITCH + bp * 4;
         *reinterpret_cast<unsigned*>(p) = h;
-        *reinterpret_cast<unsigned*>(p + bplane) = m;
-        *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
+        if (P == 3) {
+          const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
+          const unsigned m = pk_bf16(r0, r1);
+          const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
+          const unsigned l = pk_bf16(s0, s1);
+          *reinterpret_cast<unsigned*>(p + bplane) = m;
+          *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
+        }
       }
     }
   };
@@ -150,16 +154,21 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
       if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
       const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
       const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
-      bf16x8_t bf[NT][3];
+      bf16x8_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < P; ++p)
           bf[j][p] = *reinterpret_cast<const bf16x8_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
         const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+        if (P == 1) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
+          continue;
+        }
         const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
         const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
 #pragma unroll
@@ -168,7 +177,7 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
           floatx4 t = acc[i][j];
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][2], a0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
@@ -224,15 +233,19 @@ constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 static inline int x6_BM(const X6Tile& t) { return 16 * t.MT * t.WM; }
 static inline int x6_BN(const X6Tile& t) { return 16 * t.NT * t.WN; }
 static inline int x6_ncol(const X6Tile& t, int K, int s, int d) { return (x6_BN(t) - 1) * s + (K - 1) * d + 1; }
-static inline size_t x6_lds(const X6Tile& t, int ncol) {
+static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
   const size_t bplane = (size_t)((ncol * X6_PITCH + 15) / 16 * 16);
-  return 3 * bplane + 2 * 3 * (size_t)t.WM * t.MT * 1024;
+  return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
 }
 
-bool x6_cfg_valid(int cfg) { return cfg >= 100 && cfg < 100 + X6_NT; }
+// cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane)
+bool x6_cfg_valid(int cfg) { return (cfg >= 100 && cfg < 100 + X6_NT) || (cfg >= 200 && cfg < 200 + X6_NT); }
+static inline int cfg_planes(int cfg) { return cfg >= 200 ? 1 : 3; }
+static inline const X6Tile& cfg_tile(int cfg) { return kX6Tiles[cfg >= 200 ? cfg - 200 : cfg - 100]; }
 
-// Returns a x6 cfg id, or -1 when the shape should stay on the fp32 kernel.
-int x6_select_cfg(int Cout, int Cin, int K, int s, int d) {
+// Returns a x6 (planes = 3) / bf16 (planes = 1) cfg id, or -1 when the shape should stay on the
+// fp32 kernel.
+int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
   int order[6];
   int n = 0;
@@ -257,17 +270,17 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d) {
     const X6Tile& t = kX6Tiles[order[i]];
     const int ncol = x6_ncol(t, K, s, d);
     if (ncol > 32 * X6_MAXCOL_ITERS) continue;
-    if (x6_lds(t, ncol) > 160 * 1024) continue;
-    return 100 + order[i];
+    if (x6_lds(t, ncol, planes) > 160 * 1024) continue;
+    return (planes == 1 ? 200 : 100) + order[i];
   }
   return -1;
 }
 
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg) {
-  const X6Tile& t = kX6Tiles[cfg - 100];
+  const X6Tile& t = cfg_tile(cfg);
   const int ntm = (Cout + x6_BM(t) - 1) / x6_BM(t);
   const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
-  return (long long)ntm * nchunks * K * 3 * t.WM * t.MT * 1024;
+  return (long long)ntm * nchunks * K * cfg_planes(cfg) * t.WM * t.MT * 1024;
 }
 
 static inline unsigned short f2bf_rn(float f) {
@@ -286,7 +299,8 @@ static inline float bf2f(unsigned short h) {
 
 // w: [Cout][Cin][K] fp32 host -> packed bf16 planes (host), layout documented at the top.
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg) {
-  const X6Tile& t = kX6Tiles[cfg - 100];
+  const X6Tile& t = cfg_tile(cfg);
+  const int P = cfg_planes(cfg);
   const int BM = x6_BM(t), QA = t.WM * t.MT;
   const int ntm = (Cout + BM - 1) / BM;
   const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
@@ -294,7 +308,7 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
   for (int mg = 0; mg < ntm; ++mg)
     for (int c = 0; c < nchunks; ++c)
       for (int tap = 0; tap < K; ++tap)
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < P; ++p)
           for (int q = 0; q < QA; ++q)
             for (int lane = 0; lane < 64; ++lane)
               for (int j = 0; j < 8; ++j, ++o) {
@@ -311,7 +325,7 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
               }
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int P>
 static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
   const X6Tile t{MT, NT, WM, WN};
@@ -327,32 +341,36 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
   if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
-  const size_t lds = x6_lds(t, ncol);
+  const size_t lds = x6_lds(t, ncol, P);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN>), dim3(a.nwg), dim3(512), lds, st, a);
+  hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
 
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
+#define BC_X6_CASES(ID, MT, NT, WM, WN)                                \
+  case 100 + ID: return launch_x6<MT, NT, WM, WN, 3>(a, B, st);        \
+  case 200 + ID: return launch_x6<MT, NT, WM, WN, 1>(a, B, st);
   switch (cfg) {
-    case 100: return launch_x6<4, 4, 2, 4>(a, B, st);
-    case 101: return launch_x6<4, 2, 2, 4>(a, B, st);
-    case 102: return launch_x6<4, 2, 4, 2>(a, B, st);
-    case 103: return launch_x6<2, 2, 4, 2>(a, B, st);
-    case 104: return launch_x6<6, 2, 1, 8>(a, B, st);
-    case 105: return launch_x6<4, 2, 1, 8>(a, B, st);
-    case 106: return launch_x6<3, 2, 1, 8>(a, B, st);
-    case 107: return launch_x6<2, 2, 1, 8>(a, B, st);
-    case 108: return launch_x6<1, 2, 1, 8>(a, B, st);
-    case 109: return launch_x6<6, 1, 1, 8>(a, B, st);
-    case 110: return launch_x6<4, 1, 1, 8>(a, B, st);
-    case 111: return launch_x6<3, 1, 1, 8>(a, B, st);
-    case 112: return launch_x6<2, 1, 1, 8>(a, B, st);
-    case 113: return launch_x6<1, 1, 1, 8>(a, B, st);
-    case 114: return launch_x6<6, 2, 2, 4>(a, B, st);
-    case 115: return launch_x6<6, 1, 2, 4>(a, B, st);
+    BC_X6_CASES(0, 4, 4, 2, 4)
+    BC_X6_CASES(1, 4, 2, 2, 4)
+    BC_X6_CASES(2, 4, 2, 4, 2)
+    BC_X6_CASES(3, 2, 2, 4, 2)
+    BC_X6_CASES(4, 6, 2, 1, 8)
+    BC_X6_CASES(5, 4, 2, 1, 8)
+    BC_X6_CASES(6, 3, 2, 1, 8)
+    BC_X6_CASES(7, 2, 2, 1, 8)
+    BC_X6_CASES(8, 1, 2, 1, 8)
+    BC_X6_CASES(9, 6, 1, 1, 8)
+    BC_X6_CASES(10, 4, 1, 1, 8)
+    BC_X6_CASES(11, 3, 1, 1, 8)
+    BC_X6_CASES(12, 2, 1, 1, 8)
+    BC_X6_CASES(13, 1, 1, 1, 8)
+    BC_X6_CASES(14, 6, 2, 2, 4)
+    BC_X6_CASES(15, 6, 1, 2, 4)
   }
+#undef BC_X6_CASES
   return BC_ERR_ARG;
 }
 

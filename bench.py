@@ -1,14 +1,25 @@
-"""Benchmark: BASELINE.json config 2 — batch = 64 x 10 s @24 kHz clips, encode + VQ (the
-extract_indices.py path: encoder -> decoder(vq=True) -> codes) of the `default` BigCodec model on each
-GPU, fp32, synthetic white-noise clips already resident in HBM, random (counter-hash) weights.
+"""Benchmark of the BigCodec tokenization hot path on MI355X (BASELINE.json configs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model default] [--batch 64]
+Default (what the driver runs) = BASELINE config 2: batch = 64 x 10 s @24 kHz clips per GPU, encode +
+VQ (the extract_indices.py path: encoder -> decoder(vq=True) -> codes) of the `default` BigCodec
+model, fp32-accurate arithmetic, synthetic white-noise clips already resident in HBM, random
+(counter-hash) weights.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--precision fp32|x6|bf16]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
-A step = one batch per GPU through the hot path; for N > 1 each step ends with the RCCL all-gather
-of the batch's index tensor (clip-sharded data parallelism, weak scaling).  Rank 0 prints one JSON
-line with the whole-job throughput (audio-seconds encoded per second, all GPUs), the roofline of
-the dominant kernel (HIP-event timed inside the timed region) and the CPU oracle baseline.
+--config 3: full encode -> VQ -> decode round trip (inference_full.py's model path), parity adds the
+            decoder's waveform error against the CPU oracle decoding the same codes.
+--config 4: extract_indices-style corpus streaming: every step synthesises the rank's NEXT batch of
+            clips on the device, encodes + quantises it, all-gathers the indices (RCCL) and copies
+            them to the host as int16 (the .npy payload).
+--config 5: batch = 32 x 30 s per GPU with bf16 conv products (precision 'bf16'); parity reports the
+            index mismatch rate against the fp32-accurate path on the same batch.
+
+A step = one batch per GPU through the path; for N > 1 each step ends with the RCCL all-gather of the
+batch's index tensor (clip-sharded data parallelism, weak scaling).  Rank 0 prints one JSON line with
+the whole-job throughput (audio-seconds per second, all GPUs), the roofline of the dominant kernel
+(HIP-event timed inside the timed region) and the CPU oracle baseline.
 """
 from __future__ import annotations
 
@@ -22,14 +33,25 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "audio-sec encoded/sec/GPU (24 kHz mono, 10 s clips) + VQ index bit-exactness"
+METRIC_RT = "audio-sec encoded+quantised+decoded/sec (24 kHz mono, 10 s clips)"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec); 155 measured
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 X6_PRODUCTS = 6  # csrc/conv1d_x6.hip: six bf16 MFMAs per fp32-accurate product term
 HBM_PEAK_GBS = 8000.0
 
+CONFIGS = {
+    2: dict(batch=64, seconds=10.0, precision=None, work="encode+VQ (extract_indices path)"),
+    3: dict(batch=64, seconds=10.0, precision=None, work="encode+VQ+decode round trip (inference_full path)"),
+    4: dict(batch=64, seconds=10.0, precision=None,
+            work="corpus streaming: on-device clip synthesis + encode+VQ + index all-gather + int16 host copy"),
+    5: dict(batch=32, seconds=30.0, precision="bf16", work="encode+VQ, bf16 conv products"),
+}
+
 
 def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
+    if kname.startswith("conv1d_x6_kernel") and kname.endswith(", 1>"):
+        return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"
     if kname.startswith("conv1d_x6_kernel"):
         return (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS, X6_PRODUCTS,
                 "3xbf16 split: every fp32 multiply-add costs 6 bf16 MFMA multiply-adds, so the fp32-equivalent "
@@ -42,16 +64,22 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     p.add_argument("--model", default="default")
-    p.add_argument("--batch", type=int, default=64)
-    p.add_argument("--seconds", type=float, default=10.0)
+    p.add_argument("--batch", type=int, default=None, help="clips per GPU (default: the config's)")
+    p.add_argument("--seconds", type=float, default=None, help="clip length (default: the config's)")
     p.add_argument("--sample-rate", type=int, default=24000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true")
     p.add_argument("--cpu-clips", type=int, default=1)
-    p.add_argument("--precision", choices=["fp32", "x6"], default=None,
-                   help="conv GEMM arithmetic (default: BIGCODEC_PRECISION or x6)")
-    return p.parse_args()
+    p.add_argument("--precision", choices=["fp32", "x6", "bf16"], default=None,
+                   help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or x6)")
+    a = p.parse_args()
+    c = CONFIGS[a.config]
+    a.batch = a.batch or c["batch"]
+    a.seconds = a.seconds or c["seconds"]
+    a.precision = a.precision or c["precision"]
+    return a
 
 
 def build_model(name, device):
@@ -90,9 +118,10 @@ def pmc_traffic(kernel: str):
     return d["traffic_bytes_corrected"], os.path.basename(files[-1])
 
 
-def cpu_baseline(name, n_samples, sds, ek, dk, n_clips):
+def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
     """The CPU oracle (torch CPU restatement, bit-identical to the reference in the development
-    container) timed on this host: encode + VQ, B = 1 per clip (extract_indices.py:397), warm run."""
+    container) timed on this host: encode + VQ (+ decode for the round trip), B = 1 per clip
+    (extract_indices.py:397), warm run.  Returns (baseline dict, codes, waveforms or None)."""
     import torch
 
     from audiotokenization_amd import synth
@@ -101,22 +130,28 @@ def cpu_baseline(name, n_samples, sds, ek, dk, n_clips):
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
     torch.set_num_threads(threads)
     x = torch.from_numpy(synth.synth_clips(n_clips, n_samples, clip0=0)).unsqueeze(1)
-    codes = []
+    codes, wavs = [], []
     with torch.no_grad():
         O.encode_indices(x[:1, :, : n_samples // 10], sds[0], sds[1], ek, dk)  # warm-up (short)
         t0 = time.perf_counter()
         for i in range(n_clips):
-            c, _ = O.encode_indices(x[i:i + 1], sds[0], sds[1], ek, dk)
+            c, emb = O.encode_indices(x[i:i + 1], sds[0], sds[1], ek, dk)
             codes.append(c)
+            if roundtrip:
+                zq, _, _ = O.rvq_forward(emb, sds[1], "quantizer.", dk.get("vq_num_quantizers", 1))
+                wavs.append(O.decoder_forward(zq, sds[1], dk))
         dt = time.perf_counter() - t0
     audio_s = n_clips * n_samples / 24000.0
-    return dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port",
-                sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz, {name} model, encode+VQ, B=1 "
-                       f"(extract_indices.py:397), torch CPU oracle, {dt:.1f} s"), torch.cat(codes, dim=1)
+    what = "encode+VQ+decode" if roundtrip else "encode+VQ"
+    return (dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port",
+                 sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz, {name} model, {what}, B=1 "
+                        f"(extract_indices.py:397), torch CPU oracle, {dt:.1f} s"),
+            torch.cat(codes, dim=1), torch.cat(wavs, dim=0) if roundtrip else None)
 
 
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -129,7 +164,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from audiotokenization_amd import _lib
-    from audiotokenization_amd.extract import all_gather_codes, synth_batch
+    from audiotokenization_amd.extract import all_gather_codes, batch_indices_to_numpy, synth_batch
 
     _lib.load()
     if args.precision:
@@ -138,13 +173,24 @@ def main():
     n_samples = int(round(args.seconds * args.sample_rate))
     enc, dec, sds, ek, dk = build_model(args.model, dev)
     B = args.batch
+    cfgn = args.config
     x = synth_batch(B, n_samples, clip0=rank * B, device=dev)  # resident in HBM before timing
+    state = {"batch": 0, "wav": None, "host": None}
 
     def step():
         with torch.no_grad():
-            codes = dec(enc(x), vq=True)[1]
+            xb = x
+            if cfgn == 4:  # the rank's next batch of the corpus, synthesised on the device
+                xb = synth_batch(B, n_samples, clip0=(state["batch"] * world + rank) * B, device=dev)
+                state["batch"] += 1
+            post, codes, _ = dec(enc(xb), vq=True)
+            if cfgn == 3:
+                state["wav"] = dec(post, vq=False)
             if world > 1:
                 codes = all_gather_codes(codes)
+            if cfgn == 4:  # int16 payload of the .npy files, every rank's clips
+                c = codes if codes.ndim == 3 else codes.permute(1, 0, 2, 3).reshape(codes.shape[1], -1, codes.shape[3])
+                state["host"] = batch_indices_to_numpy(c)
         return codes
 
     for _ in range(args.warmup):
@@ -152,6 +198,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    state["batch"] = 0
     timer = None if args.no_kernel_timer else _lib.KernelTimer()
     _lib.set_timer(timer)
     torch.cuda.synchronize()
@@ -193,21 +240,45 @@ def main():
 
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu, codes_ref = cpu_baseline(args.model, n_samples, sds, ek, dk, args.cpu_clips)
+    if rank == 0 and cfgn == 5:
+        # index mismatch rate of the bf16 path against the fp32-accurate path on this batch
+        got = (codes[0] if world > 1 else codes)[:, :B].cpu()
+        _lib.set_precision("x6")
+        with torch.no_grad():
+            ref = dec(enc(x), vq=True)[1].cpu()
+        _lib.set_precision(args.precision)
+        parity = {"reference": "same batch through the fp32-accurate (x6) path", "frames": int(ref.numel()),
+                  "index_mismatches": int((got != ref).sum()),
+                  "mismatch_rate": round(float((got != ref).float().mean()), 5)}
+    if rank == 0 and not args.no_cpu_baseline and cfgn != 5:
+        cpu, codes_ref, wav_ref = cpu_baseline(args.model, n_samples, sds, ek, dk, args.cpu_clips,
+                                               roundtrip=cfgn == 3)
         got = codes[0] if world > 1 else codes
+        if cfgn == 4:  # the last step's batch: recompute the first clip of rank 0's batch 0
+            with torch.no_grad():
+                got = dec(enc(x), vq=True)[1]
         got = got[:, : args.cpu_clips].cpu()
         parity = {"clips_checked": args.cpu_clips, "frames": int(got.numel()),
                   "index_mismatches": int((got != codes_ref).sum())}
+        if cfgn == 3:
+            w = state["wav"][: args.cpu_clips].double().cpu()
+            r = wav_ref.double()
+            parity["waveform_mse"] = float(((w - r) ** 2).mean())
+            parity["waveform_max_abs"] = float((w - r).abs().max())
+            parity["note"] = "waveforms compared end to end; equal codes make it the decoder's error alone"
     if rank == 0:
+        dtype = {"fp32": "f32", "x6": "f32 (3xbf16-split MFMA, fp32 accumulate)",
+                 "bf16": "bf16 conv products, fp32 accumulate/storage (LSTM and VQ fp32-accurate)"}[args.precision]
+        if cfgn == 4 and state["host"] is not None:
+            assert state["host"].dtype == np.int16
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "audio-sec/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "f32 (3xbf16-split MFMA, fp32 accumulate)",
-            "data": "synthetic",
-            "config": {"workload": f"config2: batch={B} x {args.seconds:g} s {args.sample_rate // 1000} kHz clips per GPU, "
-                                   f"encode+VQ (extract_indices path), BigCodec '{args.model}' model, random weights",
+            "metric": METRIC_RT if cfgn == 3 else METRIC, "value": round(value, 2), "unit": "audio-sec/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
+            "config": {"workload": f"config{cfgn}: batch={B} x {args.seconds:g} s {args.sample_rate // 1000} kHz "
+                                   f"clips per GPU, {CONFIGS[cfgn]['work']}, BigCodec '{args.model}' model, "
+                                   f"random weights",
                        "global_batch": B * world, "clip_samples": n_samples, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
         }

@@ -41,7 +41,9 @@ int bc_abi_version(void);
  * mode 0: fp32 MFMA (v_mfma_f32_16x16x4_f32).  mode 1: fp32-accurate "x6" MFMA — both operands
  * split exactly into three bf16 terms, six bf16 products per pair accumulated in fp32 — for the
  * shapes where it applies (Cin >= 16), else the fp32 kernel.  Its error against fp64 is at or below
- * the fp32 kernel's.
+ * the fp32 kernel's.  mode 2: plain bf16 products with fp32 accumulation (one MFMA
+ * per pair; BASELINE config 5's "bf16 encoder conv stack"; activations stay fp32 in memory) where
+ * Cin >= 16, else fp32.  bc_reslstm_fwd runs mode 2 as mode 1 (the recurrence stays fp32-accurate).
  * out_snake_alpha_exp[c] = exp(alpha[c]); out_snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9).
  * Limits: Cin*Tin*4 < 2^31 bytes per clip. */
 int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode);

@@ -138,7 +138,8 @@ def test_lstm_seq_pack_layout(H):
 def test_bad_arguments_are_rejected_without_launching():
     lib = L.load()
     assert lib.bc_conv1d_select_cfg(0, 4, 7, 1, 1, 0) == -1
-    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 2) == -1  # unknown precision mode
+    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 3) == -1  # unknown precision mode
+    assert lib.bc_conv1d_select_cfg(48, 48, 7, 1, 1, 2) >= 200  # bf16 products: one-plane tiles
     assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 1) in L.CONV_CFGS  # x6 needs Cin >= 16: fp32 kernel
     assert lib.bc_conv1d_packed_floats(8, 8, 0, 0) == -1
     assert lib.bc_conv1d_fwd(None, None, None, None, None, None, None, None, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4,

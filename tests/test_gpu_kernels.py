@@ -211,6 +211,33 @@ def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
     assert errs["fp32"] < 1e-6, errs
 
 
+@pytest.mark.parametrize("Cin,Cout,K,s,d", [(384, 384, 7, 1, 9), (48, 96, 4, 2, 1), (768, 768, 1, 1, 1)])
+def test_bf16_precision_error(dev, Cin, Cout, K, s, d):
+    """precision 'bf16' (config 5): one bf16 product per pair, fp32 accumulation.  Its error against
+    fp64 is bf16-rounding sized: well below 2^-7 of the |w||x| scale, and far above the x6 path's."""
+    g = torch.Generator().manual_seed(Cin * K)
+    pad = K // 2 * d if s == 1 else s // 2 + s % 2
+    m = CV.WNConv1d(Cin, Cout, kernel_size=K, stride=s, dilation=d, padding=pad)
+    conv = _rand_wn_conv(m, g)
+    x = torch.randn(2, Cin, 400, generator=g)
+    sd = {k: v.detach() for k, v in conv.state_dict().items()}
+    w = O.wn_weight(sd, "").double()
+    y64 = F.conv1d(x.double(), w, sd["bias"].double(), s, pad, d)
+    scale = F.conv1d(x.double().abs(), w.abs(), None, s, pad, d).max()
+    m.to(dev)
+    errs = {}
+    old = L.precision_mode()
+    try:
+        for p in ("x6", "bf16"):
+            L.set_precision(p)
+            y = m.run(x.to(dev)).cpu().double()
+            errs[p] = float((y - y64).abs().max() / scale)
+    finally:
+        L._mode = old
+    assert errs["bf16"] < 2 ** -7, errs
+    assert errs["bf16"] > 50 * errs["x6"], errs  # really computed with bf16 products
+
+
 def test_vq_argmin_bit_exact(dev, golden):
     """Given the same projected latents z_e, the HIP search returns the reference's indices
     exactly, including the planted exact ties (lowest index wins) and zero / tiny rows."""
