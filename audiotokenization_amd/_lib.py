@@ -26,6 +26,8 @@ _SIGS = {
     "bc_conv1d_packed_floats": (L, [I, I, I, I]),
     "bc_conv1d_pack": (I, [P, P, I, I, I, I]),
     "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "bc_resunit_select_cfg": (I, [I, I, I]),
+    "bc_resunit_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "bc_convT1d_phase_taps": (I, [I, I]),
     "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
@@ -170,7 +172,7 @@ CONV_CFGS = {t * 4 + b: _TILES[t] + (_BKC[b],) for t in range(5) for b in range(
 X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 4, 2), (2, 2, 4, 2), (6, 2, 1, 8),
                                               (4, 2, 1, 8), (3, 2, 1, 8), (2, 2, 1, 8), (1, 2, 1, 8), (6, 1, 1, 8),
                                               (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8),
-                                              (6, 2, 2, 4), (6, 1, 2, 4)])}
+                                              (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4)])}
 
 
 def conv_kernel_name(cfg: int) -> str:
@@ -180,6 +182,11 @@ def conv_kernel_name(cfg: int) -> str:
         return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
+
+
+def resunit_kernel_name(cfg: int) -> str:
+    mt, nt, wm, wn = X6_CFGS[cfg]
+    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}>"
 
 
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6",

@@ -33,6 +33,11 @@ def _fusable(act: Optional[Activation1d]) -> bool:
     return act is not None and not act.antialias
 
 
+def _conv_of(m):
+    """The Conv1dWN behind a WNConv1d (CausalConv1d keeps it under `.conv`)."""
+    return m.conv if hasattr(m, "conv") and not hasattr(m, "weight_v") else m
+
+
 def produce_conv(conv, inp, residual=None, want_raw=True, next_act: Optional[Activation1d] = None,
                  epilogue: int = 0) -> Flow:
     """Run `conv` on an already-activated input and hand its output to `next_act`'s consumer."""
@@ -78,10 +83,49 @@ class ResidualUnit(nn.Module):
     def first_act(self) -> Activation1d:
         return self.block[0]
 
+    def _fused_cfg(self):
+        """cfg of the one-launch unit (bc_resunit_fwd), or -1 (x6 mode, no anti-aliasing, C fits)."""
+        if L.precision_mode() != 1 or self.block[2].antialias:
+            return -1
+        conv7 = _conv_of(self.block[1])
+        return L.load().bc_resunit_select_cfg(conv7.in_channels, conv7.dilation, 1)
+
     def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
         """x_act = self.first_act(x_raw) (computed by the producer)."""
+        if next_act is None or _fusable(next_act):
+            cfg = self._fused_cfg()
+            if cfg >= 0:
+                return self._flow_fused(cfg, x_raw, x_act, want_raw, next_act)
         _, h = produce_conv(self.block[1], x_act, None, want_raw=False, next_act=self.block[2])
         return produce_conv(self.block[3], h, residual=x_raw, want_raw=want_raw, next_act=next_act)
+
+    def _flow_fused(self, cfg, x_raw, x_act, want_raw, next_act) -> Flow:
+        conv7, conv1 = _conv_of(self.block[1]), _conv_of(self.block[3])
+        dev = x_act.device
+        w7, b7 = conv7.packed_as(cfg, dev)
+        w1, b1 = conv1.packed_as(cfg, dev)
+        s2a, s2b = self.block[2].act.coeffs(dev)
+        B, C, T = x_act.shape
+        if x_raw.shape != x_act.shape:
+            raise ValueError("ResidualUnit: raw and activated inputs differ in shape")
+        sa, sb = next_act.act.coeffs(dev) if next_act is not None else (None, None)
+        dual = next_act is not None and want_raw
+        y = torch.empty_like(x_act)
+        y2 = torch.empty_like(x_act) if dual else None
+        tm = L.active_timer()
+        ev = tm.begin() if tm is not None else None
+        L.call("bc_resunit_fwd", x_raw.data_ptr(), x_act.data_ptr(), w7.data_ptr(), L.ptr(b7), s2a.data_ptr(),
+               s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb), y.data_ptr(), L.ptr(y2),
+               B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_act))
+        if tm is not None:
+            flops = 2.0 * B * C * C * T * 8  # k=7 and k=1
+            nbytes = 4.0 * x_act.numel() * (3 + dual)
+            tm.end(ev, L.resunit_kernel_name(cfg), flops, nbytes)
+        if next_act is None:
+            return y, None
+        if dual:
+            return y, y2
+        return None, y
 
     def forward(self, x):
         x = _as_input(x)

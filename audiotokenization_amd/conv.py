@@ -96,6 +96,20 @@ class Conv1dWN(_WNParams, nn.Module):
             return torch.from_numpy(packed).to(device), bias, cfg
         return self._cache.get(_pkey(*self._params()) + (str(device), L.precision_mode()), build)
 
+    def packed_as(self, cfg: int, device):
+        """(packed weight, bias) for an explicit cfg (the fused ResidualUnit's tile)."""
+        def build():
+            w = self.folded_weight().contiguous()
+            Cout, Cin, K = w.shape
+            lib = L.load()
+            packed = np.empty(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg), dtype=np.float32)
+            L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, Cout, Cin, K, cfg)
+            bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
+            return torch.from_numpy(packed).to(device), bias
+        if not hasattr(self, "_cache_as"):
+            self._cache_as = _DeviceCache()
+        return self._cache_as.get(_pkey(*self._params()) + (str(device), cfg), build)
+
     def pad_left(self) -> int:
         return self.causal_pad if self.causal_pad is not None else self.padding
 

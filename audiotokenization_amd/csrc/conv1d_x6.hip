@@ -23,30 +23,16 @@
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
+#include "x6_common.h"
 
 namespace bc {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef float float2_t __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void* lds_void_t;
-
-constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
-constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
-constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352 (22 B loads / thread)
-static_assert(2 * X6_MAXCOL_ITERS == 22, "the vmcnt(22) in the main loop counts the B loads");
-
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const bf16x2_t v = __builtin_convertvector((float2_t){a, b}, bf16x2_t);
-  return __builtin_bit_cast(unsigned, v);
-}
-__device__ __forceinline__ float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
-__device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
 
 // P = operand planes: 3 (x6, fp32-accurate) or 1 (plain bf16 products: the "bf16" precision mode of
 // BASELINE config 5, activations still stored fp32).
 template <int MT, int NT, int WM, int WN, int P>
-__global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
+// NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
+// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
+__global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
@@ -206,9 +192,6 @@ __global__ void __launch_bounds__(512) conv1d_x6_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-struct X6Tile {
-  int MT, NT, WM, WN;
-};
 // cfg ids 100..: index into this table
 static const X6Tile kX6Tiles[] = {
     {4, 4, 2, 4},  // 100: BM=128 BN=256  (Cout >= 128, stride 1)
@@ -227,12 +210,11 @@ static const X6Tile kX6Tiles[] = {
     {1, 1, 1, 8},  // 113: BM=16  BN=128
     {6, 2, 2, 4},  // 114: BM=192 BN=128  (Cout = 192k, stride <= 2)
     {6, 1, 2, 4},  // 115: BM=192 BN=64
+    {3, 1, 2, 4},  // 116: BM=96  BN=64   (one-launch ResidualUnit at C = 96, two workgroups per CU)
+    {4, 1, 2, 4},  // 117: BM=128 BN=64   (two workgroups per CU)
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
-static inline int x6_BM(const X6Tile& t) { return 16 * t.MT * t.WM; }
-static inline int x6_BN(const X6Tile& t) { return 16 * t.NT * t.WN; }
-static inline int x6_ncol(const X6Tile& t, int K, int s, int d) { return (x6_BN(t) - 1) * s + (K - 1) * d + 1; }
 static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
   const size_t bplane = (size_t)((ncol * X6_PITCH + 15) / 16 * 16);
   return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
@@ -242,13 +224,41 @@ static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
 bool x6_cfg_valid(int cfg) { return (cfg >= 100 && cfg < 100 + X6_NT) || (cfg >= 200 && cfg < 200 + X6_NT); }
 static inline int cfg_planes(int cfg) { return cfg >= 200 ? 1 : 3; }
 static inline const X6Tile& cfg_tile(int cfg) { return kX6Tiles[cfg >= 200 ? cfg - 200 : cfg - 100]; }
+const X6Tile& x6_tile(int cfg) { return cfg_tile(cfg); }
 
 // Returns a x6 (planes = 3) / bf16 (planes = 1) cfg id, or -1 when the shape should stay on the
 // fp32 kernel.
+// Two-workgroup-per-CU preference: NT == 1 tiles whose LDS fits twice in a CU let one workgroup's
+// operand loads and epilogue stores overlap the other's MFMAs.  Measured on MI355X (profiles/
+// r01_occ_sweep.txt): a win for the short-K / small-M convs (Cout <= 384 with Cin*K <= 1536: the
+// C = 192 k7 and k1 convs, the C = 384 k1 conv, the stride-2 convs), a loss for the long-K ones.
+// BC_X6_OCC (tuning experiments): 4 = always try them first, 2 = never, unset = that rule.
+static int x6_occ_pref() {
+  static int v = [] {
+    const char* e = getenv("BC_X6_OCC");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
-  int order[6];
+  int order[8];
+  bool occ4[8] = {false};
   int n = 0;
+  const int pref = x6_occ_pref();
+  if (pref == 4 || (pref == 0 && Cout <= 384 && Cin * K <= 1536)) {
+    int c = -1;
+    if (Cout >= 128) c = Cout % 128 == 0 ? 17 : Cout % 96 == 0 ? 16 : -1;
+    else {
+      const int mt = (Cout + 15) / 16;
+      c = mt >= 5 ? 9 : mt == 4 ? 10 : mt == 3 ? 11 : mt == 2 ? 12 : 13;
+    }
+    if (c >= 0) {
+      occ4[n] = true;
+      order[n++] = c;
+    }
+  }
   if (Cout >= 128 && Cout % 128 != 0 && Cout % 192 == 0) {
     // 192-row tiles: no half-empty m-tile at C = 192 / 576
     if (s <= 2) order[n++] = 14;
@@ -270,7 +280,7 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
     const X6Tile& t = kX6Tiles[order[i]];
     const int ncol = x6_ncol(t, K, s, d);
     if (ncol > 32 * X6_MAXCOL_ITERS) continue;
-    if (x6_lds(t, ncol, planes) > 160 * 1024) continue;
+    if (x6_lds(t, ncol, planes) > (occ4[i] ? 80 : 160) * 1024) continue;
     return (planes == 1 ? 200 : 100) + order[i];
   }
   return -1;
@@ -369,6 +379,8 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
     BC_X6_CASES(13, 1, 1, 1, 8)
     BC_X6_CASES(14, 6, 2, 2, 4)
     BC_X6_CASES(15, 6, 1, 2, 4)
+    BC_X6_CASES(16, 3, 1, 2, 4)
+    BC_X6_CASES(17, 4, 1, 2, 4)
   }
 #undef BC_X6_CASES
   return BC_ERR_ARG;

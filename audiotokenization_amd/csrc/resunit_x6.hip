@@ -1,0 +1,331 @@
+// A whole ResidualUnit (vq/module.py:74-89) in ONE launch, fp32-accurate 3xbf16 MFMA:
+//   y = x + conv1( snake2( conv7_d( x_act ) ) )      (x_act = snake1(x), produced upstream)
+// followed by the same epilogue as a lone conv (bias, residual, optional next Snake, dual output).
+//
+// Unfused, a ResidualUnit is two launches and the k=7 conv's activated output h (C x T) makes a full
+// HBM round trip; at C <= 192 the k=1 conv is a short-K GEMM whose epilogue and staging dominate.
+// Here one workgroup owns ALL C channels of a BN-column tile:
+//   phase 1: the k=7 conv exactly as conv1d_x6_kernel's main loop (weights as the MFMA A operand, so
+//            a lane ends with 4 consecutive channels of one column);
+//   bridge : h = acc + b7, snake2, exact 3-plane bf16 split, written to LDS as the k=1 conv's input
+//            tile Hs[plane][32-ch chunk][col][32 ch] (64-B rows, 16-B groups XOR-swizzled by col so
+//            the 16 columns of a ds_read_b128 quarter-wave hit disjoint banks) - h never leaves LDS;
+//   phase 2: the k=1 conv over Hs (input as the MFMA A operand: transposed tile for the shared
+//            16-byte epilogue, conv_epilogue.h).
+// Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
+#include "bc_common.h"
+#include "bc_internal.h"
+#include "conv_epilogue.h"
+#include "x6_common.h"
+
+namespace bc {
+
+struct RUExtra {
+  const float* w1;   // packed k=1 weights
+  const float* s2a;  // Snake between the two convs: alpha_exp [C]
+  const float* s2b;  //                               inv_beta  [C]
+  int hplane;        // bytes per Hs plane = nck1 * BN * 64
+  int nck1;          // 32-channel chunks of the k=1 conv's input
+};
+
+__device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
+
+template <int MT, int NT, int WM, int WN>
+__global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
+  constexpr int BN = 16 * NT * WN;
+  constexpr int QA = WM * MT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
+
+  const int ncol = a.win;
+  const int bplane = a.bstage;
+  const int r1 = 3 * (bplane > r.hplane ? bplane : r.hplane);
+  unsigned char* Bs = smem_ru;            // phase 1: [3][ncol][80 B]
+  unsigned char* Hs = smem_ru;            // phase 2: [3][nck1][BN][64 B] (aliases Bs)
+  unsigned char* As = smem_ru + r1;       // both phases: [2][3][QA][1 KiB]
+
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int nt_idx = wg % a.ntn;
+  const int b = wg / a.ntn;
+  const int n0 = nt_idx * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+
+  const unsigned long long xb_u = (unsigned long long)(a.x + (long long)b * a.xbs);
+  const unsigned xb_lo = __builtin_amdgcn_readfirstlane((unsigned)xb_u);
+  const unsigned xb_hi = __builtin_amdgcn_readfirstlane((unsigned)(xb_u >> 32));
+  const int xbytes = __builtin_amdgcn_readfirstlane(a.Cin * a.Tin * 4);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long long)xb_hi << 32) | xb_lo), 0, xbytes, 0x00020000);
+  const int in0 = n0 - a.pl;
+
+  const int K = a.K;
+  const int nsteps = a.nchunks * K;
+  const int a_pieces = 3 * QA;
+
+  auto issue_a = [&](const float* w, int step, int buf) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)step * (a_pieces * 1024);
+    unsigned char* dst = As + buf * (a_pieces * 1024);
+    for (int q = wave; q < a_pieces; q += 8)
+      __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
+                                       16, 0, 0);
+  };
+
+  const int bp = tid >> 5;
+  const int bcl = tid & 31;
+  float bv0[X6_MAXCOL_ITERS], bv1[X6_MAXCOL_ITERS];
+  auto load_b = [&](int chunk) {
+    const int ci0 = chunk * X6_BKC + 2 * bp;
+#pragma unroll
+    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+      const int col = bcl + 32 * i;
+      const int ti = in0 + col;
+      const bool tin = col < ncol && ti >= 0 && ti < a.Tin;
+      const unsigned o0 = (tin && ci0 < a.Cin) ? (unsigned)((ci0 * a.Tin + ti) * 4) : 0xfffffff0u;
+      const unsigned o1 = (tin && ci0 + 1 < a.Cin) ? (unsigned)(((ci0 + 1) * a.Tin + ti) * 4) : 0xfffffff0u;
+      bv0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
+      bv1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
+    }
+  };
+  auto store_b = [&]() {
+#pragma unroll
+    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+      const int col = bcl + 32 * i;
+      if (col < ncol) {
+        unsigned h, m, l;
+        split2(bv0[i], bv1[i], h, m, l);
+        unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+        *reinterpret_cast<unsigned*>(p) = h;
+        *reinterpret_cast<unsigned*>(p + bplane) = m;
+        *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
+      }
+    }
+  };
+
+  // ---------------- phase 1: h = conv7(x_act), weights as the MFMA A operand ----------------
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int col_lane = wn * NT * 16 + (lane & 15);
+  const int kgrp16 = (lane >> 4) * 16;
+
+  issue_a(a.w, 0, 0);
+  load_b(0);
+  store_b();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int c = 0; c < a.nchunks; ++c) {
+    for (int tap = 0; tap < K; ++tap) {
+      const int step = c * K + tap;
+      if (step + 1 < nsteps) issue_a(a.w, step + 1, (step + 1) & 1);
+      if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
+      const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
+      const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
+      bf16x8_t bf[NT][3];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[j][p] = *reinterpret_cast<const bf16x8_t*>(Bcol + j * 16 * X6_PITCH + p * bplane);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
+        const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          floatx4 t = acc[i][j];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[j][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], t, 0, 0, 0);
+          acc[i][j] = t;
+        }
+      }
+      if (tap == K - 1 && c + 1 < a.nchunks) {
+        lds_barrier();
+        store_b();
+      }
+      if (tap == 0 && K > 1 && c + 1 < a.nchunks)
+        asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+    }
+  }
+
+  // ---------------- bridge: snake2(h + b7) -> 3 bf16 planes in LDS ----------------
+  issue_a(r.w1, 0, 0);  // the k=1 conv's first weight chunk (As is free after the last barrier)
+  const int C = a.Cout;
+  if (C < r.nck1 * X6_BKC) {  // zero the pad channels of the last chunk (never written below)
+    const int g0 = (C % X6_BKC) / 8;
+    for (int idx = tid; idx < 3 * BN * 4; idx += 512) {
+      const int p = idx / (BN * 4), n = (idx / 4) % BN, g = idx % 4;
+      if (g >= g0)
+        *reinterpret_cast<floatx4*>(Hs + p * r.hplane + (r.nck1 - 1) * (BN * 64) + hs_off(n, g)) =
+            floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int co = wm * MT * 16 + i * 16 + (lane >> 4) * 4;  // 4 consecutive channels co..co+3
+    if (co >= C) continue;
+    float bias[4], sa[4], sb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bias[q] = a.bias ? a.bias[co + q] : 0.f;
+      sa[q] = r.s2a[co + q];
+      sb[q] = r.s2b[co + q];
+    }
+    unsigned char* hrow = Hs + (co / X6_BKC) * (BN * 64) + (co % 8) * 2;
+    const int g = (co % X6_BKC) / 8;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = wn * NT * 16 + j * 16 + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = snake(acc[i][j][q] + bias[q], sa[q], sb[q]);
+      unsigned h0, m0, l0, h1, m1, l1;
+      split2(v[0], v[1], h0, m0, l0);
+      split2(v[2], v[3], h1, m1, l1);
+      unsigned char* dst = hrow + hs_off(n, g);
+      *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){h0, h1};
+      *reinterpret_cast<u32x2_t*>(dst + r.hplane) = (u32x2_t){m0, m1};
+      *reinterpret_cast<u32x2_t*>(dst + 2 * r.hplane) = (u32x2_t){l0, l1};
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+
+  // ---------------- phase 2: y = conv1(h_act), input as the MFMA A operand ----------------
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < r.nck1; ++kc) {
+    if (kc + 1 < r.nck1) issue_a(r.w1, kc + 1, (kc + 1) & 1);
+    const unsigned char* Ab = As + (kc & 1) * (a_pieces * 1024);
+    bf16x8_t bf[NT][3];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = wn * NT * 16 + j * 16 + (lane & 15);
+      const unsigned char* src = Hs + kc * (BN * 64) + hs_off(n, lane >> 4);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bf[j][p] = *reinterpret_cast<const bf16x8_t*>(src + p * r.hplane);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
+      const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        floatx4 t = acc[i][j];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][2], a0, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
+        acc[i][j] = t;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  }
+
+  conv_epilogue<MT, NT>(e, acc, b, wm * MT * 16, n0 + wn * NT * 16, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+// Candidate x6 tiles (cfg ids of conv1d_x6.hip) with one m-group covering C.  Only configurations
+// with <= 80 KB of LDS (two workgroups per CU, NT = 1 so 128 VGPRs suffice) are used: measured on
+// MI355X, the one-launch unit only beats the two separate convs when a second workgroup's MFMAs hide
+// each workgroup's operand loads and epilogue stores (at one workgroup per CU it was a wash at C = 48
+// and 96 and 8% slower at C = 192, profiles/r01_x6b_layer_profile.txt vs r01_resunit_v1_layers.txt).
+static const int kRUCandidates[] = {111, 110, 116, 112, 113};
+constexpr size_t RU_LDS_MAX = 80 * 1024;
+
+static size_t ru_lds(const X6Tile& t, int C, int d, int* bplane, int* hplane) {
+  const int ncol = x6_ncol(t, 7, 1, d);
+  *bplane = (ncol * X6_PITCH + 15) / 16 * 16;
+  *hplane = (C + X6_BKC - 1) / X6_BKC * x6_BN(t) * 64;
+  const int r1 = 3 * (*bplane > *hplane ? *bplane : *hplane);
+  return (size_t)r1 + 2 * 3 * (size_t)t.WM * t.MT * 1024;
+}
+
+int resunit_select_cfg(int C, int d, int mode) {
+  if (mode != 1 || C < 16 || C % 16 || d <= 0) return -1;
+  for (int cfg : kRUCandidates) {
+    const X6Tile& t = x6_tile(cfg);
+    if (x6_BM(t) != C) continue;
+    if (x6_ncol(t, 7, 1, d) > 32 * X6_MAXCOL_ITERS) continue;
+    int bp, hp;
+    if (ru_lds(t, C, d, &bp, &hp) > RU_LDS_MAX) continue;
+    return cfg;
+  }
+  return -1;
+}
+
+template <int MT, int NT, int WM, int WN>
+static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st) {
+  constexpr int BN = 16 * NT * WN;
+  const X6Tile t{MT, NT, WM, WN};
+  int bplane, hplane;
+  const size_t lds = ru_lds(t, a.Cout, a.d, &bplane, &hplane);
+  if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
+  a.win = x6_ncol(t, 7, 1, a.d);
+  a.bstage = bplane;
+  a.nchunks = (a.Cin + X6_BKC - 1) / X6_BKC;
+  a.ntm = 1;
+  a.ntn = (a.Nout + BN - 1) / BN;
+  r.hplane = hplane;
+  r.nck1 = (a.Cout + X6_BKC - 1) / X6_BKC;
+  const long long nwg = (long long)a.ntn * B;
+  if (nwg <= 0) return BC_OK;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  a.nwg = (int)nwg;
+  hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
+                   const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
+                   float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st) {
+  ConvArgs a{};
+  a.x = x_act; a.w = w7; a.bias = b7;
+  a.xbs = (long long)C * T;
+  a.Cin = C; a.Tin = T; a.Cout = C; a.Nout = T;
+  a.K = 7; a.s = 1; a.d = d; a.pl = pl;
+  ConvArgs e{};
+  e.bias = b1; e.res = x_raw; e.osa = osa; e.osb = osb; e.y = y; e.y2 = y2;
+  e.ybs = (long long)C * T; e.rbs = e.ybs;
+  e.Cout = C; e.Nout = T; e.yT = T; e.ostride = 1; e.ooff = 0; e.epi = 0;
+  e.vec = conv_epilogue_vec_ok(e);
+  RUExtra r{w1, s2a, s2b, 0, 0};
+  switch (cfg) {
+    case 111: return launch_ru<3, 1, 1, 8>(a, e, r, B, st);
+    case 110: return launch_ru<4, 1, 1, 8>(a, e, r, B, st);
+    case 116: return launch_ru<3, 1, 2, 4>(a, e, r, B, st);
+    case 112: return launch_ru<2, 1, 1, 8>(a, e, r, B, st);
+    case 113: return launch_ru<1, 1, 1, 8>(a, e, r, B, st);
+  }
+  return BC_ERR_ARG;
+}
+
+}  // namespace bc

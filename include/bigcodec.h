@@ -55,6 +55,22 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
                   int K, int stride, int dilation, int pad_left, int epilogue, int cfg,
                   void* stream);
 
+/* ---- ResidualUnit in one launch (mode 1 / x6 only) ---------------------------------------------
+ * Replaces ResidualUnit.forward (vq/module.py:88-89) after its first Activation1d:
+ *   v = x_raw + conv1(snake_mid(conv7_d(x_act)))      (x_act = snake1(x_raw), from the producer)
+ *   y = v, or snake_out(v), or y = v and y2 = snake_out(v)  (epilogue as bc_conv1d_fwd)
+ * x_raw, x_act, y, y2: [B][C][T]; the k=7 conv keeps length T (pad_left = 3*dilation non-causal,
+ * 6*dilation causal; the rest on the right).  w7_packed / w1_packed = bc_conv1d_pack(folded weight,
+ * K = 7 / 1, cfg) with cfg = bc_resunit_select_cfg(C, dilation, mode); that returns -1 where the
+ * unit does not fit one workgroup (then run the two bc_conv1d_fwd calls).  The activated k=7 output
+ * stays in LDS (never written to memory).  mid_snake_*: the unit's second Activation1d. */
+int bc_resunit_select_cfg(int C, int dilation, int mode);
+int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packed, const float* b7,
+                   const float* mid_snake_alpha_exp, const float* mid_snake_inv_beta,
+                   const float* w1_packed, const float* b1, const float* out_snake_alpha_exp,
+                   const float* out_snake_inv_beta, float* y, float* y2, int B, int C, int T,
+                   int dilation, int pad_left, int cfg, void* stream);
+
 /* ---- ConvTranspose1d (weight-normed, fused next-Snake epilogue) -------------------------------
  * Replaces: weight_norm(nn.ConvTranspose1d) (vq/module.py:67-72) and CausalConvTranspose1d
  * (vq/module.py:50-57, crop of the last `stride` samples) inside DecoderBlock (vq/module.py:

@@ -211,6 +211,43 @@ def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
     assert errs["fp32"] < 1e-6, errs
 
 
+@pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, False, 1, 700), (96, 3, False, 2, 513),
+                                           (64, 9, False, 2, 300), (16, 3, True, 2, 257), (64, 1, False, 1, 260),
+                                           (96, 9, True, 1, 999), (32, 1, False, 3, 64)])
+def test_resunit_fused(dev, C, d, causal, B, T):
+    """bc_resunit_fwd (one launch per ResidualUnit, x6) against the oracle: plain output, and the dual
+    raw + next-Snake output the encoder flow uses."""
+    old = L.precision_mode()
+    L.set_precision("x6")
+    try:
+        g = torch.Generator().manual_seed(C * 10 + d)
+        ru = BL.ResidualUnit(C, dilation=d, causal=causal)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            s = _snake(C, g)
+            ru.block[k].act.load_state_dict(s.state_dict())
+        nxt = M.Activation1d(activation=_snake(C, g))
+        x = torch.randn(B, C, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        want = O.residual_unit(x, sd, "", d, causal, False)
+        want_s = O.snake_beta(want, nxt.act.alpha.detach(), nxt.act.beta.detach())
+        ru.to(dev)
+        nxt.to(dev)
+        assert ru._fused_cfg() >= 0
+        xd = x.to(dev)
+        xa = ru.first_act(xd)
+        got = ru.flow(xd, xa)[0].cpu()
+        raw, act = ru.flow(xd, xa, want_raw=True, next_act=nxt)
+        _, act_only = ru.flow(xd, xa, want_raw=False, next_act=nxt)
+    finally:
+        L._mode = old
+    assert_close_rel(got, want, 2e-5, f"resunit C={C} d={d}")
+    assert torch.equal(raw.cpu(), got)
+    assert_close_rel(act.cpu(), want_s, 5e-5, "resunit + next snake")
+    assert torch.equal(act_only.cpu(), act.cpu())
+
+
 @pytest.mark.parametrize("Cin,Cout,K,s,d", [(384, 384, 7, 1, 9), (48, 96, 4, 2, 1), (768, 768, 1, 1, 1)])
 def test_bf16_precision_error(dev, Cin, Cout, K, s, d):
     """precision 'bf16' (config 5): one bf16 product per pair, fp32 accumulation.  Its error against

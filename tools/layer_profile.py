@@ -60,11 +60,26 @@ def main():
         rows.append((f"ResLSTM H={H} T={T} layers={self.lstm.num_layers}", fl, e0, e1))
         return y
 
+    rorig = BLK.ResidualUnit._flow_fused
+
+    def timed_ru(self, cfg, x_raw, x_act, want_raw, next_act):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = rorig(self, cfg, x_raw, x_act, want_raw, next_act)
+        e1.record()
+        B, C, T = x_act.shape
+        conv7 = BLK._conv_of(self.block[1])
+        rows.append((f"resunit C={C} d={conv7.dilation} T={T}{' dual' if want_raw and next_act else ''}",
+                     2.0 * B * C * C * T * 8, e0, e1))
+        return out
+
     with torch.no_grad():
         dec(enc(x), vq=True)  # warm-up / weight prep
         torch.cuda.synchronize()
         CV.Conv1dWN.run = timed_run
         BLK.ResLSTM.run = timed_lstm
+        BLK.ResidualUnit._flow_fused = timed_ru
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
