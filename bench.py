@@ -105,17 +105,16 @@ def build_model(name, device):
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (tools/gpu_pmc.sh ->
-    tools/pmc_summary.py -> profiles/*pmc_traffic.json), or (None, None)."""
+    """(HBM bytes per launch, MFMA utilisation, source file) of `kernel` from the newest committed PMC
+    summary (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/*pmc_traffic.json), or Nones."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))["kernels"].get(kernel)
-    if not d:
-        return None, None
-    return d["traffic_bytes_corrected"], os.path.basename(files[-1])
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        d = json.load(open(f))["kernels"].get(kernel)
+        if d:
+            return d["traffic_bytes_corrected"], d.get("mfma_util"), os.path.basename(f)
+    return None, None, None
 
 
 def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
@@ -226,12 +225,13 @@ def main():
         avg_ms = d["ms_total"] / d["launches"]
         achieved = d["flops_total"] / d["launches"] / (avg_ms * 1e-3) / 1e12
         conv_ms = sum(v["ms_total"] for v in summ.values())
-        traffic, tsrc = pmc_traffic(kname)
+        traffic, mutil, tsrc = pmc_traffic(kname)
         peak, mult, note = kernel_peak(kname)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "peak_note": note,
                 "mfma_tflops_executed": round(achieved * mult, 2),
                 "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+                "pmc_mfma_util": round(mutil, 4) if mutil is not None else None,
                 "algorithmic_bytes_per_launch": round(d["bytes_total"] / d["launches"]), "kernel": kname,
                 "launches_per_step": d["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_gflop_per_launch": round(d["flops_total"] / d["launches"] / 1e9, 3),

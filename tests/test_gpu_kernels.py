@@ -207,6 +207,8 @@ def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
             errs[p] = float((y - y64).abs().max() / scale)
     finally:
         L._mode = old
+    print(f"conv {Cin}->{Cout} k{K} d{d}: max|y - y64| / max(sum|w x|): fp32 MFMA {errs['fp32']:.3e}, "
+          f"x6 {errs['x6']:.3e}")
     assert errs["x6"] <= 1.25 * errs["fp32"] + 1e-9, errs
     assert errs["fp32"] < 1e-6, errs
 
@@ -271,6 +273,7 @@ def test_bf16_precision_error(dev, Cin, Cout, K, s, d):
             errs[p] = float((y - y64).abs().max() / scale)
     finally:
         L._mode = old
+    print(f"conv {Cin}->{Cout} k{K} s{s} d{d}: relative error x6 {errs['x6']:.3e}, bf16 {errs['bf16']:.3e}")
     assert errs["bf16"] < 2 ** -7, errs
     assert errs["bf16"] > 50 * errs["x6"], errs  # really computed with bf16 products
 

@@ -1,47 +1,69 @@
-"""Summarise rocprofv3 PMC passes (tools/gpu_pmc.sh) into per-kernel HBM traffic per launch.
+"""Summarise rocprofv3 PMC passes (tools/gpu_pmc.sh) into per-kernel HBM traffic and MFMA
+utilisation per launch.
 
     python tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc_traffic.json
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md §HBM, on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read; WRITE_SIZE is exact
-for streaming stores.  A calibration on this code's own 4-B-per-lane transpose kernel (known bytes)
-is recorded beside the result, and the traffic figure applies the guide's x2 read correction (an
-upper bound for kernels whose reads are partly 4-B wide)."""
+for streaming stores.  traffic = 2 * FETCH_SIZE + WRITE_SIZE (the guide's x2 read correction; an
+upper bound for kernels whose reads are partly 4-B wide).
+
+MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): the busy
+cycles of the matrix pipes (16 per v_mfma_f32_16x16x32_bf16, checked against the algorithmic MFMA
+count of the C = 384 k=7 conv) over the SIMD-cycles the dispatch was resident, at the clock it ran."""
 import collections
 import csv
 import json
 import os
 import sys
 
+N_XCD, N_SIMD = 8, 1024
 
-def load(path):
+
+def load(path, counter=None):
     out = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return out
     for r in csv.DictReader(open(path)):
+        if counter and r["Counter_Name"] != counter:
+            continue
         name = r["Kernel_Name"]
         if name.startswith("void "):
             name = name[5:]
         name = name.split("(")[0].replace("bc::", "")
-        out[name].append(float(r["Counter_Value"]) * 1024.0)
+        out[name].append(float(r["Counter_Value"]))
     return out
+
+
+def mean(v):
+    return sum(v) / len(v) if v else 0.0
 
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     fetch = load(os.path.join(src, "FETCH_SIZE", "run_counter_collection.csv"))
     write = load(os.path.join(src, "WRITE_SIZE", "run_counter_collection.csv"))
+    mp = os.path.join(src, "MFMA", "run_counter_collection.csv")
+    busy = load(mp, "SQ_VALU_MFMA_BUSY_CYCLES")
+    gui = load(mp, "GRBM_GUI_ACTIVE")
     res = {}
     for k in fetch:
-        f = sum(fetch[k]) / len(fetch[k])
-        w = sum(write.get(k, [0.0])) / max(1, len(write.get(k, [0.0])))
-        res[k] = {"launches": len(fetch[k]), "fetch_bytes_raw": f, "write_bytes": w,
-                  "traffic_bytes_corrected": 2.0 * f + w}
-    out = {"note": "per-launch averages; traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 wide-read correction)",
+        f = mean(fetch[k]) * 1024.0
+        w = mean(write.get(k, [])) * 1024.0
+        d = {"launches": len(fetch[k]), "fetch_bytes_raw": f, "write_bytes": w,
+             "traffic_bytes_corrected": 2.0 * f + w}
+        if busy.get(k) and gui.get(k):
+            util = [b / (g / N_XCD * N_SIMD) for b, g in zip(busy[k], gui[k]) if g > 0]
+            d["mfma_util"] = mean(util)
+            d["mfma_busy_cycles"] = mean(busy[k])
+        res[k] = d
+    out = {"note": "per-launch averages; traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 wide-read correction); "
+                   "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
            "kernels": res}
-    calib = res.get("btc_to_ctb_kernel")
-    if calib:
-        out["calibration_btc_to_ctb"] = {"fetch_raw_over_known": None, "write_raw_bytes": calib["write_bytes"]}
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
-    print(json.dumps({k: round(v["traffic_bytes_corrected"] / 1e9, 3) for k, v in res.items()}, indent=1))
+    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["traffic_bytes_corrected"] * kv[1]["launches"]):
+        print(f"{k:60s} x{v['launches']:3d}  traffic {v['traffic_bytes_corrected'] / 1e9:8.3f} GB/launch"
+              + (f"  mfma_util {v['mfma_util']:.3f}" if "mfma_util" in v else ""))
 
 
 if __name__ == "__main__":
