@@ -16,9 +16,10 @@
 // Arithmetic: the fp32-accurate 3xbf16 split of conv1d_x6.hip (six bf16 MFMAs per product term);
 //   h is split on the fly, W_hh on the host.  The four waves' partial sums are reduced through LDS
 //   in a fixed order, then c = f*c + i*g, h = o*tanh(c) with c held in registers.
-// Hand-off of h_t: the workgroup gathers its 8 units x 64 clips in LDS, one wave writes them with
-//   16-byte write-through (sc1) stores into slot t of the fragment-native sequence buffer
-//   hseq[t][k-step][n-tile][lane][8], drains them (vmcnt(0)) and one lane stores flags[g] = t+1
+// Hand-off of h_t: the workgroup gathers its 8 units x 64 clips in LDS, one wave splits them into
+//   the three bf16 planes and writes them with 16-byte write-through (sc1) stores into slot t of the
+//   fragment-native sequence buffer hseq[t][k-step][n-tile][plane][lane][8 bf16] (the consumers'
+//   MFMA B fragments as they are), drains them (vmcnt(0)) and one lane stores flags[g] = t+1
 //   (relaxed, agent scope).  Consumer wave w polls the flags of the G/4 workgroups that produce its
 //   K range (sc1 loads, bounded spin), then reads slot t-1 with PLAIN loads: every slot is written
 //   once per launch and read only after its flag, so no L1/L2 of this launch can hold an older
@@ -42,8 +43,10 @@ typedef __attribute__((address_space(1))) unsigned ls_gu32;
 constexpr int LS_U = 8;          // hidden units per workgroup
 constexpr int LS_WAVES = 4;
 constexpr int LS_NB = 64;        // clips per launch (4 n-tiles of 16)
+constexpr int LS_HSTEP_PER_UNIT = LS_NB * 3 / 2;  // floats of hseq per hidden unit per step (3 bf16 planes)
 constexpr int LS_SC1 = 16;       // buffer-op cache policy: sc1 (write-through / L1 bypass)
 constexpr unsigned LS_SPIN_LIMIT = 1u << 22;
+constexpr int LS_FLAG_BYTES = 2 * 256 * 4;  // flags[half][workgroup], G <= 256
 
 struct LstmSeqArgs {
   const float* gx;            // [4H][T*Btot] input projection incl. b_ih + b_hh (ctb layout)
@@ -54,7 +57,10 @@ struct LstmSeqArgs {
   int* status;                // timeout counter (0 = ok)
   int H, T, Btot, b0, nb;
   int dbg;  // timing experiments only (BC_LSTM_SEQ_DEBUG): 4 = skip the flag poll (wrong results)
+  long long* stamps;  // diagnostic s_memtime stamps (BC_LSTM_SEQ_STAMPS), nullptr in normal runs
 };
+
+constexpr int LS_STAMP_T = 2048;  // steps recorded per stamped workgroup
 
 __device__ __forceinline__ unsigned ls_pk(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector((ls_float2){a, b}, ls_bf16x2));
@@ -76,6 +82,13 @@ __device__ __forceinline__ void ls_split8(const float (&v)[8], ls_bf16x8 (&p)[3]
   p[1] = __builtin_bit_cast(ls_bf16x8, (ls_u32x4){m[0], m[1], m[2], m[3]});
   p[2] = __builtin_bit_cast(ls_bf16x8, (ls_u32x4){l[0], l[1], l[2], l[3]});
 }
+
+// Cell nonlinearities on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each): the
+// OCML expf / division / tanhf versions took 2200 of a step's 30 000 cycles (stamped timeline,
+// tools/lstm_bench.py).  tanh(x) = 1 - 2 / (1 + e^{2x}) saturates exactly to +-1 and has an absolute
+// error ~1e-7 near 0, the fp32-class error the recurrence test bounds.
+__device__ __forceinline__ float ls_sigmoid(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float ls_tanh(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ls_rsrc(const void* p, unsigned bytes) {
   const unsigned long long u = (unsigned long long)p;
@@ -121,7 +134,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
   }
   float cst[2] = {0.f, 0.f};
 
-  const long long hstep = (long long)H * LS_NB;  // floats of h per step in hseq
+  const long long hstep = (long long)H * LS_HSTEP_PER_UNIT;  // floats of hseq per step
   const int nprod = G / LS_WAVES;                // producers of this wave's K range
   ls_gu32* flags = (ls_gu32*)(a.flags);
 
@@ -139,7 +152,14 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
   float gxv[2][4], gxn[2][4];
   load_gx(0, gxv);
 
+  // diagnostic timeline of workgroups 0 and G/2: [wg][t][wave][event]
+  long long* stamp_row = nullptr;
+  if (a.stamps && lane == 0 && (g == 0 || g == G / 2)) stamp_row = a.stamps + (long long)(g == 0 ? 0 : 1) * LS_STAMP_T * 32;
+#define LS_STAMP(ev)                                                                             \
+  if (stamp_row && t < LS_STAMP_T) stamp_row[(t * 4 + w) * 8 + (ev)] = (long long)__builtin_amdgcn_s_memtime();
+
   for (int t = 0; t < a.T; ++t) {
+    LS_STAMP(0)
 
     floatx4 acc[2][4];
 #pragma unroll
@@ -165,37 +185,32 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
         __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
+      LS_STAMP(1)
       // h_{t-1} lives at addresses no cache of this launch has seen before it was written through
       // (one slot per step), so plain L2-cached loads are fresh and the XCD's L2 serves its CUs.
-      // Register double buffer: the 8 loads of k-step ks+1 are in flight while k-step ks runs its
-      // 48 MFMAs (one wave per SIMD: nothing else hides the L2 latency).
-      const floatx4* hp = reinterpret_cast<const floatx4*>(a.hseq + (long long)(t - 1) * hstep) + lane * 2;
-      floatx4 hbuf[2][4][2];
-      auto load_ks = [&](int ks, floatx4 (&dst)[4][2]) {
+      // h arrives already split into its three bf16 planes (the producer splits once), as MFMA B
+      // fragments: 3 x 16 B per lane per (k-step, n-tile).  Register double buffer: the 12 loads of
+      // k-step ks+1 are in flight while k-step ks runs its 48 MFMAs (one wave per SIMD: nothing else
+      // hides the L2 latency).
+      const ls_bf16x8* hp = reinterpret_cast<const ls_bf16x8*>(a.hseq + (long long)(t - 1) * hstep) + lane;
+      ls_bf16x8 hbuf[2][4][3];
+      auto load_ks = [&](int ks, ls_bf16x8 (&dst)[4][3]) {
         const int ksa = w * KS + ks;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          dst[nt][0] = hp[(ksa * 4 + nt) * 128];
-          dst[nt][1] = hp[(ksa * 4 + nt) * 128 + 1];
-        }
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) dst[nt][p] = hp[((ksa * 4 + nt) * 3 + p) * 64];
       };
       load_ks(0, hbuf[0]);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         if (ks + 1 < KS) load_ks(ks + 1, hbuf[(ks + 1) & 1]);
         // keep the scheduler from sinking those loads to their uses (it does under this register
-        // pressure, serialising 96 L2 round trips per step)
+        // pressure, serialising 144 L2 round trips per step)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          float hv[8];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            hv[i] = hbuf[ks & 1][nt][0][i];
-            hv[4 + i] = hbuf[ks & 1][nt][1][i];
-          }
-          ls_bf16x8 hb[3];
-          ls_split8(hv, hb);
+          const ls_bf16x8* hb = hbuf[ks & 1][nt];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
             floatx4 s = acc[mt][nt];
@@ -212,11 +227,13 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
     }
 
     // ---- reduce the four waves' partial sums (fixed order), cell update ----
+    LS_STAMP(2)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) red[w][mt * 4 + nt][lane] = acc[mt][nt];
     __syncthreads();
+    LS_STAMP(3)
     if (bail) return;  // uniform: every wave reads it after the same barrier
     float hq[2];
 #pragma unroll
@@ -232,34 +249,38 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
       float gt[4];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) gt[gate] = t > 0 ? gxv[q][gate] + hsum[gate] : gxv[q][gate];
-      const float ig = sigmoidf_ref(gt[0]);
-      const float fg = sigmoidf_ref(gt[1]);
-      const float gg = tanhf(gt[2]);
-      const float og = sigmoidf_ref(gt[3]);
+      const float ig = ls_sigmoid(gt[0]);
+      const float fg = ls_sigmoid(gt[1]);
+      const float gg = ls_tanh(gt[2]);
+      const float og = ls_sigmoid(gt[3]);
       const float c = fg * cst[q] + ig * gg;
       cst[q] = c;
-      hq[q] = cb[q] < a.nb ? og * tanhf(c) : 0.f;
+      hq[q] = cb[q] < a.nb ? og * ls_tanh(c) : 0.f;
       hs[cb[q]][cu[q]] = hq[q];
     }
+    LS_STAMP(4)
     __syncthreads();
+    LS_STAMP(5)
 
-    // ---- publish h_t: wave 0, one clip per lane, 32 B write-through, drained, then the flag ----
+    // ---- publish h_t: wave 0, one clip per lane: split once into the three bf16 planes (the
+    //      consumers' MFMA B fragments), 3 x 16 B write-through, drained, then the flag ----
     if (w == 0 && t + 1 < a.T) {
       const int b = lane, nt = b >> 4, c16 = b & 15;
       const int ksa = g >> 2, qq = g & 3;
       const __amdgpu_buffer_rsrc_t hr = ls_rsrc(a.hseq + (long long)t * hstep, (unsigned)(hstep * 4));
-      const unsigned off = (unsigned)(((ksa * 4 + nt) * 64 + qq * 16 + c16) * 32);
-      ls_u32x4 v0, v1;
+      const unsigned off = (unsigned)((ksa * 4 + nt) * 3 * 1024 + (qq * 16 + c16) * 16);
+      float hv[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v0[i] = __float_as_uint(hs[b][i]);
-        v1[i] = __float_as_uint(hs[b][4 + i]);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, v0), hr, off, 0, LS_SC1);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, v1), hr, off + 16, 0, LS_SC1);
+      for (int i = 0; i < 8; ++i) hv[i] = hs[b][i];
+      ls_bf16x8 pl[3];
+      ls_split8(hv, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, pl[p]), hr, off + p * 1024, 0, LS_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(flags + g, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    LS_STAMP(6)
     // layer output (read only after the launch): off the publishing wave's critical path
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -274,6 +295,191 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
         for (int gate = 0; gate < 4; ++gate) gxv[q][gate] = gxn[q][gate];
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Two interleaved half-batches (default).  The 64 clips of a launch are two independent
+// recurrences of 32 clips; every workgroup alternates half 0 and half 1, so the hand-off of one
+// half's h_t (write-through, flag, other workgroups' polls, fabric fetch: ~5 us, stamped timeline
+// in DESIGN.md) overlaps the MFMAs of the other half instead of stalling the whole step.  The
+// publishing wave also defers its flag store (and the drain before it) until after the next
+// half-step's MFMAs, when the write-through stores have long completed.
+//   hseq[t][half][k-step][n-tile (2)][plane][lane][8 bf16]; flags[half][G]; one cell per thread per
+//   half (tile p = wave: m-tile p>>1, n-tile p&1).
+// ------------------------------------------------------------------------------------------------
+template <int KS>
+__global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
+  constexpr int NH = 32;                       // clips per half
+  __shared__ floatx4 red[LS_WAVES][4][64];     // per-wave partial gates of one half's 4 tiles
+  __shared__ float hs[NH][LS_U + 1];           // one half's h_t gathered per clip
+  __shared__ int bail;
+
+  const int g = blockIdx.x;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H;
+  const long long TB = (long long)a.T * a.Btot;
+  if (tid == 0) bail = 0;
+
+  ls_bf16x8 wr[2][KS][3];
+  {
+    const ls_bf16x8* wp = reinterpret_cast<const ls_bf16x8*>(a.whh) + (long long)(g * LS_WAVES + w) * (2 * KS * 3) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wr[mt][ks][p] = wp[((mt * KS + ks) * 3 + p) * 64];
+  }
+
+  const int cu = (w >> 1) * 4 + (lane >> 4);   // my cell's unit within the workgroup
+  const int cbh = (w & 1) * 16 + (lane & 15);  // my cell's clip within a half
+  float cst0 = 0.f, cst1 = 0.f;                // my cell's c in half 0 / half 1
+
+  const long long hhalf = (long long)H * (LS_HSTEP_PER_UNIT / 2);  // floats of hseq per half-step
+  const int nprod = G / LS_WAVES;
+  ls_gu32* flags = (ls_gu32*)(a.flags);
+  int pend_h = -1;        // wave 0: half whose h stores are issued but whose flag is not yet set
+  unsigned pend_v = 0;
+
+  long long* stamp_row = nullptr;
+  if (a.stamps && lane == 0 && (g == 0 || g == G / 2)) stamp_row = a.stamps + (long long)(g == 0 ? 0 : 1) * LS_STAMP_T * 32;
+
+  for (int t = 0; t < a.T; ++t) {
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      const int ts = 2 * t + h;  // stamp row
+#define LS2_STAMP(ev) \
+  if (stamp_row && ts < LS_STAMP_T) stamp_row[(ts * 4 + w) * 8 + (ev)] = (long long)__builtin_amdgcn_s_memtime();
+      LS2_STAMP(0)
+      const int clip = h * NH + cbh;
+      const bool ok = clip < a.nb;
+      float gxv[4];
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate)
+        gxv[gate] = ok ? a.gx[((long long)gate * H + g * LS_U + cu) * TB + (long long)t * a.Btot + a.b0 + clip] : 0.f;
+
+      floatx4 acc[2][2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+      if (t > 0) {
+        const ls_gu32* fl = flags + h * 256 + w * nprod;
+        unsigned spins = 0;
+        while (!(a.dbg & 4)) {
+          const unsigned f = lane < nprod ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0xffffffffu;
+          if (__all(f >= (unsigned)t)) break;
+          if (++spins > LS_SPIN_LIMIT) {
+            if (lane == 0) {
+              atomicAdd(a.status, 1);
+              bail = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        LS2_STAMP(1)
+        const ls_bf16x8* hp =
+            reinterpret_cast<const ls_bf16x8*>(a.hseq + ((long long)(t - 1) * 2 + h) * hhalf) + lane;
+        ls_bf16x8 hbuf[2][2][3];
+        auto load_ks = [&](int ks, ls_bf16x8 (&dst)[2][3]) {
+          const int ksa = w * KS + ks;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) dst[nt][p] = hp[((ksa * 2 + nt) * 3 + p) * 64];
+        };
+        load_ks(0, hbuf[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) load_ks(ks + 1, hbuf[(ks + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const ls_bf16x8* hb = hbuf[ks & 1][nt];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+              floatx4 s = acc[mt][nt];
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][2], hb[0], s, 0, 0, 0);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][1], hb[1], s, 0, 0, 0);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[2], s, 0, 0, 0);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][1], hb[0], s, 0, 0, 0);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[1], s, 0, 0, 0);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[0], s, 0, 0, 0);
+              acc[mt][nt] = s;
+            }
+          }
+        }
+      }
+      LS2_STAMP(2)
+      // deferred flag of the previous half-step's publish: its stores were issued a whole
+      // half-step ago, so this drain is (nearly) free
+      if (w == 0 && pend_h >= 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(flags + pend_h * 256 + g, pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend_h = -1;
+      }
+
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) red[w][mt * 2 + nt][lane] = acc[mt][nt];
+      __syncthreads();
+      LS2_STAMP(3)
+      if (bail) return;
+      floatx4 hsum = red[0][w][lane];
+#pragma unroll
+      for (int ww = 1; ww < LS_WAVES; ++ww) {
+        const floatx4 r = red[ww][w][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hsum[i] = hsum[i] + r[i];
+      }
+      float gt[4];
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate) gt[gate] = t > 0 ? gxv[gate] + hsum[gate] : gxv[gate];
+      const float ig = ls_sigmoid(gt[0]);
+      const float fg = ls_sigmoid(gt[1]);
+      const float gg = ls_tanh(gt[2]);
+      const float og = ls_sigmoid(gt[3]);
+      const float c = fg * (h ? cst1 : cst0) + ig * gg;
+      if (h) cst1 = c;
+      else cst0 = c;
+      const float hq = ok ? og * ls_tanh(c) : 0.f;
+      hs[cbh][cu] = hq;
+      LS2_STAMP(4)
+      __syncthreads();
+      LS2_STAMP(5)
+
+      if (w == 0 && t + 1 < a.T && lane < NH) {
+        const int nt = lane >> 4, c16 = lane & 15;
+        const int ksa = g >> 2, qq = g & 3;
+        const __amdgpu_buffer_rsrc_t hr =
+            ls_rsrc(a.hseq + ((long long)t * 2 + h) * hhalf, (unsigned)(hhalf * 4));
+        const unsigned off = (unsigned)((ksa * 2 + nt) * 3 * 1024 + (qq * 16 + c16) * 16);
+        float hv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hv[i] = hs[lane][i];
+        ls_bf16x8 pl[3];
+        ls_split8(hv, pl);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, pl[p]), hr, off + p * 1024, 0, LS_SC1);
+      }
+      if (w == 0 && t + 1 < a.T) {
+        pend_h = h;
+        pend_v = (unsigned)(t + 1);
+      }
+      LS2_STAMP(6)
+      if (ok) a.y[(long long)(g * LS_U + cu) * TB + (long long)t * a.Btot + a.b0 + clip] = hq;
+#undef LS2_STAMP
+    }
+  }
+  // no flag can still be pending: the last step publishes nothing
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -325,7 +531,7 @@ void lstm_seq_pack(const float* w, unsigned short* out, int H) {
 }
 
 long long lstm_seq_workspace_bytes(int H, int T) {
-  return 1024 + (long long)T * H * LS_NB * 4;  // flags (<= 256 words) | hseq
+  return LS_FLAG_BYTES + (long long)T * H * LS_HSTEP_PER_UNIT * 4;  // flags [2][256] | hseq
 }
 
 __device__ int bc_lstm_seq_timeouts;  // bumped by a workgroup that gave up waiting (never in a good run)
@@ -347,6 +553,17 @@ int lstm_seq_read_status(int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(bc_lstm_seq_timeouts), &z, sizeof(int)) != hipSuccess) return -1;
   }
   return v;
+}
+
+// Diagnostic stamp buffer (BC_LSTM_SEQ_STAMPS=1): allocated once, read by bc_debug_lstm_stamps.
+static long long* lstm_seq_stamp_buffer() {
+  static long long* p = [] {
+    const char* e = getenv("BC_LSTM_SEQ_STAMPS");
+    long long* q = nullptr;
+    if (e && atoi(e) && hipMalloc(&q, sizeof(long long) * 2 * LS_STAMP_T * 32) != hipSuccess) q = nullptr;
+    return q;
+  }();
+  return p;
 }
 
 static int device_cus() {
@@ -371,7 +588,7 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
   a.whh = whh;
   a.y = y;
   a.flags = reinterpret_cast<unsigned*>(ws);
-  a.hseq = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + 1024);
+  a.hseq = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + LS_FLAG_BYTES);
   a.status = status;
   a.H = H;
   a.T = T;
@@ -381,20 +598,42 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
     return e ? atoi(e) : 0;
   }();
   a.dbg = dbg;
+  a.stamps = lstm_seq_stamp_buffer();
+  // BC_LSTM_SEQ_HALVES=1: the single-batch kernel (kept for A/B timing), else two interleaved halves
+  static const bool halves = [] {
+    const char* e = getenv("BC_LSTM_SEQ_HALVES");
+    return !(e && atoi(e) == 1);
+  }();
   for (int b0 = 0; b0 < Btot; b0 += LS_NB) {
     a.b0 = b0;
     a.nb = Btot - b0 < LS_NB ? Btot - b0 : LS_NB;
-    if (hipMemsetAsync(a.flags, 0, 1024, st) != hipSuccess) return BC_ERR_LAUNCH;
+    if (hipMemsetAsync(a.flags, 0, LS_FLAG_BYTES, st) != hipSuccess) return BC_ERR_LAUNCH;
+#define BC_LS_CASE(KS)                                                                      \
+  case KS:                                                                                  \
+    if (halves)                                                                             \
+      hipLaunchKernelGGL(lstm_seq2_x6_kernel<KS>, dim3(G), dim3(256), 0, st, a);            \
+    else                                                                                    \
+      hipLaunchKernelGGL(lstm_seq_x6_kernel<KS>, dim3(G), dim3(256), 0, st, a);             \
+    break;
     switch (H / 128) {
-      case 2: hipLaunchKernelGGL(lstm_seq_x6_kernel<2>, dim3(G), dim3(256), 0, st, a); break;
-      case 4: hipLaunchKernelGGL(lstm_seq_x6_kernel<4>, dim3(G), dim3(256), 0, st, a); break;
-      case 8: hipLaunchKernelGGL(lstm_seq_x6_kernel<8>, dim3(G), dim3(256), 0, st, a); break;
-      case 12: hipLaunchKernelGGL(lstm_seq_x6_kernel<12>, dim3(G), dim3(256), 0, st, a); break;
+      BC_LS_CASE(2)
+      BC_LS_CASE(4)
+      BC_LS_CASE(8)
+      BC_LS_CASE(12)
       default: return BC_ERR_UNSUPPORTED;
     }
+#undef BC_LS_CASE
     BC_CHECK_LAUNCH();
   }
   return BC_OK;
 }
 
 }  // namespace bc
+
+// Diagnostics only (not part of include/bigcodec.h): copy the last persistent launch's stamps
+// [2 workgroups][2048 steps][4 waves][8 events] (s_memtime ticks) to the host; synchronises.
+extern "C" int bc_debug_lstm_stamps(long long* host, long long n) {
+  long long* p = bc::lstm_seq_stamp_buffer();
+  if (!p || !host || n <= 0 || n > 2LL * bc::LS_STAMP_T * 32) return 1;
+  return hipMemcpy(host, p, sizeof(long long) * n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}

@@ -50,6 +50,37 @@ def main():
     print(f"H={a.H} B={a.B} T={a.T} layers={a.layers} prec={a.precision} "
           f"dbg={os.environ.get('BC_LSTM_SEQ_DEBUG', '0')}: {dt * 1e3:.2f} ms "
           f"({dt * 1e6 / (a.T * a.layers):.2f} us/step incl. input projection) status={st}", flush=True)
+    if os.environ.get("BC_LSTM_SEQ_STAMPS"):
+        timeline(a.T)
+
+
+def timeline(T):
+    """Per-step phase durations (s_memtime ticks) of workgroups 0 and G/2 from the last launch:
+    0 step start, 1 poll done, 2 MFMAs done, 3 reduction barrier passed, 4 cell done,
+    5 gather barrier passed, 6 publish done (wave 0)."""
+    import ctypes as C
+
+    lib = L.load()
+    n = 2 * 2048 * 32
+    buf = (C.c_longlong * n)()
+    fn = lib.bc_debug_lstm_stamps
+    fn.argtypes = [C.c_void_p, C.c_longlong]
+    if fn(C.addressof(buf), n) != 0:
+        print("no stamps")
+        return
+    if os.environ.get("BC_LSTM_SEQ_HALVES", "2") != "1":
+        T = min(2048, 2 * T)  # rows are half-steps (2t + half)
+        print("rows = half-steps")
+    s = np.frombuffer(buf, dtype=np.int64).reshape(2, 2048, 4, 8)[:, :T]
+    names = ["poll", "load+mfma", "red.barrier", "cell", "gather.barrier", "publish", "tail->next"]
+    lo, hi = 10, T - 10
+    for wgi in range(2):
+        step = s[wgi, lo + 1:hi + 1, 0, 0] - s[wgi, lo:hi, 0, 0]
+        print(f"workgroup {'0' if wgi == 0 else 'G/2'}: step {np.median(step):.0f} ticks (median)")
+        for w in range(4):
+            d = [np.median(s[wgi, lo:hi, w, k + 1] - s[wgi, lo:hi, w, k]) for k in range(6)]
+            d.append(np.median(s[wgi, lo + 1:hi + 1, w, 0] - s[wgi, lo:hi, w, 6]))
+            print(f"  wave {w}: " + "  ".join(f"{nm} {v:6.0f}" for nm, v in zip(names, d)))
 
 
 if __name__ == "__main__":
