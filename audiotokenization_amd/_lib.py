@@ -176,6 +176,7 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
 
 
 def conv_kernel_name(cfg: int) -> str:
+    cfg = cfg % 1000 if cfg >= 1000 else cfg  # phase-decomposed strided convs run the same kernels
     if cfg in X6_CFGS or cfg - 100 in X6_CFGS:
         planes = 3 if cfg in X6_CFGS else 1
         mt, nt, wm, wn = X6_CFGS[cfg if planes == 3 else cfg - 100]

@@ -17,6 +17,10 @@ struct ConvArgs {
   int K, s, d, pl;
   int yT, ostride, ooff;
   int epi;             // 0 none, 1 tanh
+  // phase decomposition of a strided conv (x6 kernel, cfg >= 1000): the kernel runs the stride-1
+  // conv over ps * cin0 phase channels ci' = ci * ps + r, x_r[ci][m] = x[ci][m * ps + r - pl]
+  int ps;              // 0: off
+  int cin0;            // real input channels when ps != 0
   // filled by conv_launch
   int vec;             // 16-byte epilogue accesses allowed (conv_epilogue_vec_ok)
   int nchunks, win, bstage, astage;

@@ -19,6 +19,7 @@
 //                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
 //                at tap 0 and land while the current chunk's taps compute.
 #include <cstring>
+#include <vector>
 
 #include "bc_common.h"
 #include "bc_internal.h"
@@ -60,10 +61,11 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   const unsigned long long xb_u = (unsigned long long)(a.x + (long long)b * a.xbs);
   const unsigned xb_lo = __builtin_amdgcn_readfirstlane((unsigned)xb_u);
   const unsigned xb_hi = __builtin_amdgcn_readfirstlane((unsigned)(xb_u >> 32));
-  const int xbytes = __builtin_amdgcn_readfirstlane(a.Cin * a.Tin * 4);
+  const int xbytes = __builtin_amdgcn_readfirstlane((a.ps ? a.cin0 : a.Cin) * a.Tin * 4);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(((unsigned long long)xb_hi << 32) | xb_lo), 0, xbytes, 0x00020000);
   const int in0 = n0 * a.s - a.pl;
+  const int tstep = a.ps ? a.ps : 1;  // input samples per B-tile column
 
   const int K = a.K;
   const int nsteps = a.nchunks * K;
@@ -85,13 +87,23 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   float bv0[X6_MAXCOL_ITERS], bv1[X6_MAXCOL_ITERS];
   auto load_b = [&](int chunk) {
     const int ci0 = chunk * X6_BKC + 2 * bp;
+    // channel (row) -> input channel and the input time of column 0; phase mode: row ci' is phase
+    // r = ci' % ps of channel ci' / ps, column m reads sample (n0 + m) * ps + r - pl
+    int ch0 = ci0, ch1 = ci0 + 1, tb0 = in0, tb1 = in0;
+    if (a.ps) {
+      ch0 = ci0 / a.ps;
+      ch1 = (ci0 + 1) / a.ps;
+      tb0 = n0 * a.ps + (ci0 - ch0 * a.ps) - a.pl;
+      tb1 = n0 * a.ps + (ci0 + 1 - ch1 * a.ps) - a.pl;
+    }
 #pragma unroll
     for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
       const int col = bcl + 32 * i;
-      const int ti = in0 + col;
-      const bool tin = col < ncol && ti >= 0 && ti < a.Tin;
-      const unsigned o0 = (tin && ci0 < a.Cin) ? (unsigned)((ci0 * a.Tin + ti) * 4) : 0xfffffff0u;
-      const unsigned o1 = (tin && ci0 + 1 < a.Cin) ? (unsigned)(((ci0 + 1) * a.Tin + ti) * 4) : 0xfffffff0u;
+      const int t0 = tb0 + col * tstep, t1 = tb1 + col * tstep;
+      const bool cin = col < ncol;
+      const unsigned o0 = (cin && ci0 < a.Cin && t0 >= 0 && t0 < a.Tin) ? (unsigned)((ch0 * a.Tin + t0) * 4) : 0xfffffff0u;
+      const unsigned o1 =
+          (cin && ci0 + 1 < a.Cin && t1 >= 0 && t1 < a.Tin) ? (unsigned)((ch1 * a.Tin + t1) * 4) : 0xfffffff0u;
       bv0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
       bv1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
     }
@@ -220,10 +232,22 @@ static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
   return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
 }
 
-// cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane)
-bool x6_cfg_valid(int cfg) { return (cfg >= 100 && cfg < 100 + X6_NT) || (cfg >= 200 && cfg < 200 + X6_NT); }
-static inline int cfg_planes(int cfg) { return cfg >= 200 ? 1 : 3; }
-static inline const X6Tile& cfg_tile(int cfg) { return kX6Tiles[cfg >= 200 ? cfg - 200 : cfg - 100]; }
+// cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane); + 1000 * s for a stride-s
+// conv run by phase decomposition (ConvArgs::ps): the stride-1 conv with ceil(K/s) taps over s * Cin
+// phase channels ci' = ci * s + r, weights W'[co][ci'][q] = W[co][ci][q * s + r] (0 past K).  Its
+// input tile needs BN + ceil(K/s) - 1 columns instead of (BN - 1) * s + K, so the wide 128 x 256
+// tile fits the stride-4/5 convs.
+static inline int cfg_base(int cfg) { return cfg % 1000; }
+static inline int cfg_phase(int cfg) { return cfg / 1000; }
+bool x6_cfg_valid(int cfg) {
+  const int b = cfg_base(cfg), s = cfg_phase(cfg);
+  return ((b >= 100 && b < 100 + X6_NT) || (b >= 200 && b < 200 + X6_NT)) && (s == 0 || (s >= 2 && s <= 16));
+}
+static inline int cfg_planes(int cfg) { return cfg_base(cfg) >= 200 ? 1 : 3; }
+static inline const X6Tile& cfg_tile(int cfg) {
+  const int b = cfg_base(cfg);
+  return kX6Tiles[b >= 200 ? b - 200 : b - 100];
+}
 const X6Tile& x6_tile(int cfg) { return cfg_tile(cfg); }
 
 // Returns a x6 (planes = 3) / bf16 (planes = 1) cfg id, or -1 when the shape should stay on the
@@ -241,8 +265,28 @@ static int x6_occ_pref() {
   return v;
 }
 
+static int x6_select_tile(int Cout, int Cin, int K, int s, int d, int planes);
+
+// Stride >= 3 convs with dilation 1 (the encoder's k=2s downsampling) run phase-decomposed
+// (BC_X6_PHASE=0 disables it for A/B timing).
+static bool x6_phase_ok(int s, int d) {
+  static int v = [] {
+    const char* e = getenv("BC_X6_PHASE");
+    return e ? atoi(e) : 1;
+  }();
+  return v && s >= 3 && s <= 16 && d == 1;
+}
+
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
+  if (x6_phase_ok(s, d)) {
+    const int c = x6_select_tile(Cout, Cin * s, (K + s - 1) / s, 1, 1, planes);
+    if (c >= 0) return 1000 * s + c;
+  }
+  return x6_select_tile(Cout, Cin, K, s, d, planes);
+}
+
+static int x6_select_tile(int Cout, int Cin, int K, int s, int d, int planes) {
   int order[8];
   bool occ4[8] = {false};
   int n = 0;
@@ -288,6 +332,10 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
 
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg) {
   const X6Tile& t = cfg_tile(cfg);
+  if (const int s = cfg_phase(cfg)) {
+    Cin *= s;
+    K = (K + s - 1) / s;
+  }
   const int ntm = (Cout + x6_BM(t) - 1) / x6_BM(t);
   const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
   return (long long)ntm * nchunks * K * cfg_planes(cfg) * t.WM * t.MT * 1024;
@@ -309,6 +357,16 @@ static inline float bf2f(unsigned short h) {
 
 // w: [Cout][Cin][K] fp32 host -> packed bf16 planes (host), layout documented at the top.
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg) {
+  if (const int s = cfg_phase(cfg)) {  // phase-decomposed weights W'[co][ci * s + r][q]
+    const int Kp = (K + s - 1) / s, Cp = Cin * s;
+    std::vector<float> wp((size_t)Cout * Cp * Kp, 0.f);
+    for (int co = 0; co < Cout; ++co)
+      for (int ci = 0; ci < Cin; ++ci)
+        for (int k = 0; k < K; ++k)
+          wp[((size_t)co * Cp + ci * s + k % s) * Kp + k / s] = w[((size_t)co * Cin + ci) * K + k];
+    x6_pack_weight(wp.data(), out, Cout, Cp, Kp, cfg_base(cfg));
+    return;
+  }
   const X6Tile& t = cfg_tile(cfg);
   const int P = cfg_planes(cfg);
   const int BM = x6_BM(t), QA = t.WM * t.MT;
@@ -349,7 +407,7 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   const long long nwg = (long long)a.ntm * a.ntn * B;
   if (nwg <= 0) return BC_OK;
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
-  if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  if ((long long)(a.ps ? a.cin0 : a.Cin) * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
   const size_t lds = x6_lds(t, ncol, P);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
@@ -359,6 +417,16 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
 }
 
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
+  a.ps = 0;
+  if (const int s = cfg_phase(cfg)) {  // run as the stride-1 conv over the s phases
+    if (a.s != s || a.d != 1 || a.ostride != 1) return BC_ERR_ARG;
+    a.ps = s;
+    a.cin0 = a.Cin;
+    a.Cin *= s;
+    a.K = (a.K + s - 1) / s;
+    a.s = 1;
+    cfg = cfg_base(cfg);
+  }
 #define BC_X6_CASES(ID, MT, NT, WM, WN)                                \
   case 100 + ID: return launch_x6<MT, NT, WM, WN, 3>(a, B, st);        \
   case 200 + ID: return launch_x6<MT, NT, WM, WN, 1>(a, B, st);
