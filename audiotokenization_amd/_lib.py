@@ -175,12 +175,16 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
                                               (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4)])}
 
 
-def conv_kernel_name(cfg: int) -> str:
-    cfg = cfg % 1000 if cfg >= 1000 else cfg  # phase-decomposed strided convs run the same kernels
+def conv_kernel_name(cfg: int, taps: int = 0) -> str:
+    """Kernel symbol a conv launch with this cfg runs (`taps` = kernel size after any phase
+    decomposition: the x6 kernel has a pointwise variant for 1)."""
+    if cfg >= 1000:  # phase-decomposed strided convs run the same kernels with ceil(K/s) taps
+        taps = -(-taps // (cfg // 1000))
+        cfg %= 1000
     if cfg in X6_CFGS or cfg - 100 in X6_CFGS:
         planes = 3 if cfg in X6_CFGS else 1
         mt, nt, wm, wn = X6_CFGS[cfg if planes == 3 else cfg - 100]
-        return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}>"
+        return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, {'true' if taps == 1 else 'false'}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
 

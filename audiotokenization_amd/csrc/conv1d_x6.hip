@@ -30,13 +30,15 @@ namespace bc {
 
 // P = operand planes: 3 (x6, fp32-accurate) or 1 (plain bf16 products: the "bf16" precision mode of
 // BASELINE config 5, activations still stored fp32).
-template <int MT, int NT, int WM, int WN, int P>
+// PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
+template <int MT, int NT, int WM, int WN, int P, bool PW>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
 // one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
+  constexpr int CI = PW ? BN / 32 : X6_MAXCOL_ITERS;  // 32-column B passes per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
 
   const int ncol = a.win;                // columns of the input tile
@@ -81,11 +83,11 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
                                        16, 0, 0);
   };
 
-  // B staging: thread -> (channel pair p, column lane cl); columns cl + 32*i
+  // B staging: thread -> (channel pair p, column lane cl); columns cl + 32*i, i < CI
   const int bp = tid >> 5;       // 0..15
   const int bcl = tid & 31;
-  float bv0[X6_MAXCOL_ITERS], bv1[X6_MAXCOL_ITERS];
-  auto load_b = [&](int chunk) {
+  float bv0[CI], bv1[CI];
+  auto load_b = [&](int chunk, float (&v0)[CI], float (&v1)[CI]) {
     const int ci0 = chunk * X6_BKC + 2 * bp;
     // channel (row) -> input channel and the input time of column 0; phase mode: row ci' is phase
     // r = ci' % ps of channel ci' / ps, column m reads sample (n0 + m) * ps + r - pl
@@ -97,23 +99,23 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       tb1 = n0 * a.ps + (ci0 + 1 - ch1 * a.ps) - a.pl;
     }
 #pragma unroll
-    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+    for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       const int t0 = tb0 + col * tstep, t1 = tb1 + col * tstep;
       const bool cin = col < ncol;
       const unsigned o0 = (cin && ci0 < a.Cin && t0 >= 0 && t0 < a.Tin) ? (unsigned)((ch0 * a.Tin + t0) * 4) : 0xfffffff0u;
       const unsigned o1 =
           (cin && ci0 + 1 < a.Cin && t1 >= 0 && t1 < a.Tin) ? (unsigned)((ch1 * a.Tin + t1) * 4) : 0xfffffff0u;
-      bv0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
-      bv1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
+      v0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
+      v1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
     }
   };
-  auto store_b = [&]() {
+  auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI]) {
 #pragma unroll
-    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+    for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       if (col < ncol) {
-        const float v0 = bv0[i], v1 = bv1[i];
+        const float v0 = w0[i], v1 = w1[i];
         const unsigned h = pk_bf16(v0, v1);
         unsigned char* p = Bs + col * X6_PITCH + bp * 4;
         *reinterpret_cast<unsigned*>(p) = h;
@@ -138,18 +140,8 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
   const int kgrp16 = (lane >> 4) * 16;
 
-  // prologue: A(step 0), B(chunk 0)
-  issue_a(0, 0);
-  load_b(0);
-  store_b();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int c = 0; c < a.nchunks; ++c) {
-    for (int tap = 0; tap < K; ++tap) {
-      const int step = c * K + tap;
-      if (step + 1 < nsteps) issue_a(step + 1, (step + 1) & 1);
-      if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
+  // one K32 step: this wave's MT x NT tiles += A(step) * B(tap-shifted columns)
+  auto compute = [&](int step, int tap) {
       const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
       const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
       bf16x8_t bf[NT][P];
@@ -182,23 +174,64 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
           acc[i][j] = t;
         }
       }
-      if (tap == K - 1 && c + 1 < a.nchunks) {
+  };
+
+  // prologue: A(step 0), B(chunk 0)
+  issue_a(0, 0);
+  load_b(0, bv0, bv1);
+  store_b(bv0, bv1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  if constexpr (PW) {
+    // Pointwise conv (K = 1): one step per chunk, so the B loads run two chunks ahead in two
+    // register sets (chunk c + 2 is issued while chunk c computes and chunk c + 1 is stored).
+    float bw0[CI], bw1[CI];
+    if (a.nchunks > 1) load_b(1, bw0, bw1);
+    auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
+      if (c + 1 < a.nchunks && !(a.dbg & 1)) issue_a(c + 1, (c + 1) & 1);
+      if (c + 2 < a.nchunks && !(a.dbg & 2)) load_b(c + 2, p0v, p1v);
+      compute(c, 0);
+      if (c + 1 < a.nchunks) {
         lds_barrier();  // every wave is done reading this chunk's B tile
-        store_b();
+        if (!(a.dbg & 4)) store_b(n0v, n1v);
       }
-      // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
-      // tap 0 of a multi-tap chunk the 2*X6_MAXCOL_ITERS B loads of the next chunk were issued
-      // after it and may stay in flight (vmcnt retires in issue order); they are consumed at the
-      // chunk's last tap, where the compiler waits for their registers itself.
-      if (tap == 0 && K > 1 && c + 1 < a.nchunks)
-        asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+      // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
+      if (c + 2 < a.nchunks)
+        wait_vmcnt<2 * CI>();
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
+    };
+    for (int c = 0; c < a.nchunks; c += 2) {
+      step1(c, bw0, bw1, bv0, bv1);
+      if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
+    }
+  } else {
+    for (int c = 0; c < a.nchunks; ++c) {
+      for (int tap = 0; tap < K; ++tap) {
+        const int step = c * K + tap;
+        if (step + 1 < nsteps && !(a.dbg & 1)) issue_a(step + 1, (step + 1) & 1);
+        if (tap == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
+        compute(step, tap);
+        if (tap == K - 1 && c + 1 < a.nchunks) {
+          lds_barrier();  // every wave is done reading this chunk's B tile
+          if (!(a.dbg & 4)) store_b(bv0, bv1);
+        }
+        // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
+        // tap 0 of a multi-tap chunk the 2*CI B loads of the next chunk were issued after it and
+        // may stay in flight (vmcnt retires in issue order); they are consumed at the chunk's last
+        // tap, where the compiler waits for their registers itself.
+        if (tap == 0 && K > 1 && c + 1 < a.nchunks)
+          wait_vmcnt<2 * CI>();
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+      }
     }
   }
 
-  conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
+  if (!(a.dbg & 8)) conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -277,8 +310,39 @@ static bool x6_phase_ok(int s, int d) {
   return v && s >= 3 && s <= 16 && d == 1;
 }
 
+// Measured tile preferences of the x6 (three-plane) kernel, from a sweep of every tile over the
+// BigCodec encoder's conv shapes (tools/conv_bench.py --cfg all, profiles/r01_tile_sweep.txt):
+//   pointwise, Cout % 128 == 0     -> 101 (128 x 128, two-chunk B prefetch): C = 384 / 768 and the
+//                                     LSTM input projection 1536 -> 6144, 12-24 % under the others
+//   pointwise, Cout % 96 == 0      -> 116 (96 x 64, two workgroups per CU): C = 192
+//   stride 1, K > 1, Cout % 96 == 0 and <= 384 -> 109 (96 x 128, all 8 waves on one 96-row block,
+//                                     two workgroups per CU): k7 C = 192 -17 %, C = 384 -2 %
+//   stride 2, Cout % 96 == 0 and <= 192 -> phase-decomposed 109: the k4 downsampling at C = 48 / 96
+//                                     -33 % / -7 %
+// Returns the cfg or -1 (then the general rules below decide).
+static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
+  auto fits2 = [](int tile, int K_, int s_, int d_) {  // two workgroups per CU: LDS <= 80 KiB
+    const X6Tile& t = kX6Tiles[tile];
+    const int ncol = x6_ncol(t, K_, s_, d_);
+    return ncol <= 32 * X6_MAXCOL_ITERS && x6_lds(t, ncol, 3) <= 80 * 1024;
+  };
+  if (s == 1 && K == 1) {
+    if (Cout % 128 == 0) return 101;
+    if (Cout % 96 == 0) return 116;
+    return -1;
+  }
+  if (s == 1 && Cout % 96 == 0 && Cout <= 384 && fits2(9, K, 1, d)) return 109;
+  if (s == 2 && d == 1 && Cout % 96 == 0 && Cout <= 192 && Cin * 2 >= 32 && fits2(9, (K + 1) / 2, 1, 1))
+    return 2000 + 109;
+  return -1;
+}
+
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
+  if (planes == 3 && x6_occ_pref() == 0) {
+    const int c = x6_preferred_cfg(Cout, Cin, K, s, d);
+    if (c >= 0) return c;
+  }
   if (x6_phase_ok(s, d)) {
     const int c = x6_select_tile(Cout, Cin * s, (K + s - 1) / s, 1, 1, planes);
     if (c >= 0) return 1000 * s + c;
@@ -393,6 +457,15 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
               }
 }
 
+// BC_X6_PW=0 runs pointwise convs on the general kernel (A/B timing).
+static bool x6_pw_on() {
+  static const bool v = [] {
+    const char* e = getenv("BC_X6_PW");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 template <int MT, int NT, int WM, int WN, int P>
 static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
@@ -411,12 +484,20 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   a.nwg = (int)nwg;
   const size_t lds = x6_lds(t, ncol, P);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a);
+  if (a.K == 1 && ncol == BN && x6_pw_on())
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
+  else
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), lds, st, a);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
 
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
+  static const int dbg = [] {
+    const char* e = getenv("BC_X6_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
   a.ps = 0;
   if (const int s = cfg_phase(cfg)) {  // run as the stride-1 conv over the s phases
     if (a.s != s || a.d != 1 || a.ostride != 1) return BC_ERR_ARG;

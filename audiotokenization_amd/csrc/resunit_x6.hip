@@ -20,6 +20,8 @@
 
 namespace bc {
 
+constexpr int RU_MAX_DIL = 9;  // the B loads are sized for the k7 halo at dilation <= 9 (BigCodec: 1, 3, 9)
+
 struct RUExtra {
   const float* w1;   // packed k=1 weights
   const float* s2a;  // Snake between the two convs: alpha_exp [C]
@@ -34,6 +36,7 @@ template <int MT, int NT, int WM, int WN>
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;
+  constexpr int CI = (BN + 6 * RU_MAX_DIL + 31) / 32;  // 32-column B passes: ncol <= BN + 6 * d
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
 
   const int ncol = a.win;
@@ -76,11 +79,11 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 
   const int bp = tid >> 5;
   const int bcl = tid & 31;
-  float bv0[X6_MAXCOL_ITERS], bv1[X6_MAXCOL_ITERS];
+  float bv0[CI], bv1[CI];
   auto load_b = [&](int chunk) {
     const int ci0 = chunk * X6_BKC + 2 * bp;
 #pragma unroll
-    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+    for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       const int ti = in0 + col;
       const bool tin = col < ncol && ti >= 0 && ti < a.Tin;
@@ -92,7 +95,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   };
   auto store_b = [&]() {
 #pragma unroll
-    for (int i = 0; i < X6_MAXCOL_ITERS; ++i) {
+    for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       if (col < ncol) {
         unsigned h, m, l;
@@ -157,7 +160,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         store_b();
       }
       if (tap == 0 && K > 1 && c + 1 < a.nchunks)
-        asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+        wait_vmcnt<2 * CI>();
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
@@ -272,7 +275,7 @@ int resunit_select_cfg(int C, int d, int mode) {
   for (int cfg : kRUCandidates) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
-    if (x6_ncol(t, 7, 1, d) > 32 * X6_MAXCOL_ITERS) continue;
+    if (d > RU_MAX_DIL) return -1;
     int bp, hp;
     if (ru_lds(t, C, d, &bp, &hp) > RU_LDS_MAX) continue;
     return cfg;

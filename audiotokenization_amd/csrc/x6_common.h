@@ -17,7 +17,13 @@ typedef __attribute__((address_space(3))) void* lds_void_t;
 constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
 constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
 constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352 (22 B loads / thread)
-static_assert(2 * X6_MAXCOL_ITERS == 22, "the vmcnt(22) in the main loop counts the B loads");
+
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding: vmcnt[3:0] + [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   const bf16x2_t v = __builtin_convertvector((float2_t){a, b}, bf16x2_t);

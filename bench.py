@@ -50,7 +50,8 @@ CONFIGS = {
 
 def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
-    if kname.startswith("conv1d_x6_kernel") and kname.endswith(", 1>"):
+    targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
+    if kname.startswith("conv1d_x6_kernel") and len(targs) >= 5 and targs[4] == "1":  # P = 1 plane
         return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"
     if kname.startswith("conv1d_x6_kernel"):
         return (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS, X6_PRODUCTS,

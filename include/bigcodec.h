@@ -37,7 +37,8 @@ int bc_abi_version(void);
  * pad_left = (K - stride) * dilation (vq/module.py:43).  The input x is the already-activated
  * tensor (the Snake that precedes every reference conv runs in the producer's epilogue or in
  * bc_snake_fwd).  W is the FOLDED weight g*v/||v|| [Cout][Cin][K] packed by bc_conv1d_pack for
- * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode).
+ * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode) (any other valid tile id also
+ * runs — tuning — with weights packed for that same cfg; a tile the shape does not fit returns 3).
  * mode 0: fp32 MFMA (v_mfma_f32_16x16x4_f32).  mode 1: fp32-accurate "x6" MFMA — both operands
  * split exactly into three bf16 terms, six bf16 products per pair accumulated in fp32 — for the
  * shapes where it applies (Cin >= 16), else the fp32 kernel.  Its error against fp64 is at or below

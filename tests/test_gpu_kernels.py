@@ -361,6 +361,7 @@ def test_synth_clips_device_equals_host(dev):
 
 def test_abi_rejects_bad_args(dev):
     lib = L.load()
-    # wrong cfg for the shape -> BC_ERR_ARG, nothing launched
-    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 0, None) == 1
+    # invalid cfg id, or a phase-decomposed cfg for another stride -> BC_ERR_ARG, nothing launched
+    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 99, None) == 1
+    assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 5109, None) == 1
     assert lib.bc_vq_argmin(1, 1, 1, 1, 10, 8192, 4, None) == 3
