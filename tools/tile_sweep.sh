@@ -1,3 +1,4 @@
+# Tile sweep of the encoder conv shapes (every x6 cfg per shape): profiles/r01_tile_sweep.txt
 set -e
 mkdir -p gpurun_out
 run() { timeout -k 10 300 python tools/conv_bench.py --iters 5 --cfg all "$@" >> gpurun_out/sweep.log 2>&1; }
