@@ -35,6 +35,7 @@ _SIGS = {
     "bc_lstm_hh_packed_floats": (L, [I, I]),
     "bc_lstm_pack_hh": (I, [P, P, I, I]),
     "bc_lstm_status": (I, [I]),
+    "bc_mfma_probe": (I, [P, I, I, P]),
     "bc_lstm_workspace_floats": (L, [I, I, I]),
     "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),

@@ -154,6 +154,8 @@ long long bc_lstm_hh_packed_floats(int H, int mode) {
 
 int bc_lstm_status(int reset) { return lstm_seq_read_status(reset); }
 
+int bc_mfma_probe(float* out, int nwg, int iters, void* stream) { return mfma_probe_launch(out, nwg, iters, S(stream)); }
+
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode) {
   if (!w_hh_host || !packed_host || H <= 0 || H % 16 || mode < 0 || mode > 2) return BC_ERR_ARG;
   if (lstm_use_seq(H, mode))

@@ -52,6 +52,36 @@ __device__ __forceinline__ float snake(float x, float alpha_exp, float inv_beta)
   return x + inv_beta * (s * s);
 }
 
+// The same two functions on pairs, written so the fp32 arithmetic issues as packed v_pk_fma_f32 /
+// v_pk_mul_f32 / v_pk_add_f32 (two lanes' worth of work per instruction: the epilogues that apply
+// a Snake to every output element are VALU-heavy).  Each component rounds exactly as bc_sin /
+// snake above (same operations, same order), so the results are bit-identical to them.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
+__device__ __forceinline__ f32x2 bc_sin_pk(f32x2 x) {
+  const f32x2 t = x * splat2(0.318309886183790671538f);
+  const f32x2 q = {rintf(t.x), rintf(t.y)};
+  f32x2 d = __builtin_elementwise_fma(q, splat2(-3.140625f), x);
+  d = __builtin_elementwise_fma(q, splat2(-0.0009670257568359375f), d);
+  d = __builtin_elementwise_fma(q, splat2(-6.2771141529083251953e-07f), d);
+  d = __builtin_elementwise_fma(q, splat2(-1.2154201256553420762e-10f), d);
+  const f32x2 s = d * d;
+  if (((int)q.x) & 1) d.x = -d.x;
+  if (((int)q.y) & 1) d.y = -d.y;
+  f32x2 u = splat2(2.6083159809786593541503e-06f);
+  u = __builtin_elementwise_fma(u, s, splat2(-0.0001981069071916863322258f));
+  u = __builtin_elementwise_fma(u, s, splat2(0.00833307858556509017944336f));
+  u = __builtin_elementwise_fma(u, s, splat2(-0.166666597127914428710938f));
+  f32x2 r = __builtin_elementwise_fma(s, u * d, d);
+  if (!(fabsf(x.x) < 39000.0f)) r.x = sinf(x.x);
+  if (!(fabsf(x.y) < 39000.0f)) r.y = sinf(x.y);
+  return r;
+}
+__device__ __forceinline__ f32x2 snake_pk(f32x2 x, f32x2 alpha_exp, f32x2 inv_beta) {
+  const f32x2 s = bc_sin_pk(x * alpha_exp);
+  return x + inv_beta * (s * s);
+}
+
 // Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): workgroups that the dispatcher deals to the same XCD (ids b, b+8, b+16, ...) receive
 // consecutive logical ids, so neighbouring tiles that share an input panel share one L2.

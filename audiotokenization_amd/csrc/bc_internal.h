@@ -70,6 +70,8 @@ int lstm_seq_read_status(int reset);
 int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
                      int T, int t, hipStream_t st);
 
+int mfma_probe_launch(float* out, int nwg, int iters, hipStream_t st);
+
 int vq_prepare_launch(const float* cb, float* cbn, float* csq, int n, hipStream_t st);
 int vq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* cb,
                   const float* cbn, const float* csq, const float* w_out, const float* b_out,

@@ -49,9 +49,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
         if (rb) r = *reinterpret_cast<const floatx4*>(rb + yi);
         floatx4 v, sv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[q] = conv_epi_value(a, acc[i][j][q], bias, r[q], rb != nullptr);
-          sv[q] = snk ? snake(v[q], sa, sb) : v[q];
+        for (int q = 0; q < 4; ++q) v[q] = conv_epi_value(a, acc[i][j][q], bias, r[q], rb != nullptr);
+        if (snk) {
+          const f32x2 lo = snake_pk((f32x2){v[0], v[1]}, splat2(sa), splat2(sb));
+          const f32x2 hi = snake_pk((f32x2){v[2], v[3]}, splat2(sa), splat2(sb));
+          sv = (floatx4){lo.x, lo.y, hi.x, hi.y};
+        } else {
+          sv = v;
         }
         if (y2b) {
           *reinterpret_cast<floatx4*>(yb + yi) = v;

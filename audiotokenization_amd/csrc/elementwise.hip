@@ -18,10 +18,18 @@ namespace bc {
 __global__ void snake_kernel(const float* __restrict__ x, const float* __restrict__ sa,
                              const float* __restrict__ sb, float* __restrict__ y, int C, long long T,
                              long long total) {
+  // element pairs through the packed Snake (the one every conv epilogue runs); an odd tail alone
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c = (int)((i / T) % C);
-    y[i] = snake(x[i], sa[c], sb[c]);
+  for (long long i = 2 * ((long long)blockIdx.x * blockDim.x + threadIdx.x); i < total; i += 2 * stride) {
+    const int c0 = (int)((i / T) % C);
+    if (i + 1 < total) {
+      const int c1 = (int)(((i + 1) / T) % C);
+      const f32x2 v = snake_pk((f32x2){x[i], x[i + 1]}, (f32x2){sa[c0], sa[c1]}, (f32x2){sb[c0], sb[c1]});
+      y[i] = v.x;
+      y[i + 1] = v.y;
+    } else {
+      y[i] = snake(x[i], sa[c0], sb[c0]);
+    }
   }
 }
 

@@ -196,8 +196,11 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
     for (int j = 0; j < NT; ++j) {
       const int n = wn * NT * 16 + j * 16 + (lane & 15);
       float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = snake(acc[i][j][q] + bias[q], sa[q], sb[q]);
+      const f32x2 lo = snake_pk((f32x2){acc[i][j][0] + bias[0], acc[i][j][1] + bias[1]}, (f32x2){sa[0], sa[1]},
+                                (f32x2){sb[0], sb[1]});
+      const f32x2 hi = snake_pk((f32x2){acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]}, (f32x2){sa[2], sa[3]},
+                                (f32x2){sb[2], sb[3]});
+      v[0] = lo.x, v[1] = lo.y, v[2] = hi.x, v[3] = hi.y;
       unsigned h0, m0, l0, h1, m1, l1;
       split2(v[0], v[1], h0, m0, l0);
       split2(v[2], v[3], h1, m1, l1);

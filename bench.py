@@ -118,6 +118,25 @@ def pmc_traffic(kernel: str):
     return None, None, None
 
 
+def mfma_probe_tflops(dev, nwg=2048, iters=60000):
+    """Dense BF16 MFMA rate this device sustains on random register operands (bc_mfma_probe: no
+    memory, four waves per SIMD on every CU), in TFLOP/s: the practical ceiling under the chip's
+    clock management, beside the 2.5 PFLOP/s spec peak (MI355X_MICROARCH.md 'DVFS give-back')."""
+    import torch
+
+    from audiotokenization_amd import _lib
+
+    out = torch.empty(nwg * 4, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    _lib.call("bc_mfma_probe", out.data_ptr(), nwg, iters // 3, st)  # warm, clock settles
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _lib.call("bc_mfma_probe", out.data_ptr(), nwg, iters, st)
+    e1.record()
+    torch.cuda.synchronize()
+    return nwg * 4 * iters * 16 * 16384.0 / (e0.elapsed_time(e1) * 1e-3) / 1e12
+
+
 def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
     """The CPU oracle (torch CPU restatement, bit-identical to the reference in the development
     container) timed on this host: encode + VQ (+ decode for the round trip), B = 1 per clip
@@ -228,8 +247,15 @@ def main():
         conv_ms = sum(v["ms_total"] for v in summ.values())
         traffic, mutil, tsrc = pmc_traffic(kname)
         peak, mult, note = kernel_peak(kname)
+        probe = mfma_probe_tflops(dev)
+        practical = probe / mult if kname.startswith("conv1d_x6_kernel") else None
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "peak_note": note,
+                "probe_bf16_tflops": round(probe, 1),
+                "practical_peak": round(practical, 2) if practical else None,
+                "practical_frac": round(achieved / practical, 4) if practical else None,
+                "practical_note": "bc_mfma_probe: the dense-BF16 rate this device sustains on random register "
+                                  "operands (its clock under MFMA load), / the kernel's MFMAs per FLOP pair",
                 "mfma_tflops_executed": round(achieved * mult, 2),
                 "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
                 "pmc_mfma_util": round(mutil, 4) if mutil is not None else None,

@@ -118,6 +118,12 @@ long long bc_lstm_hh_packed_floats(int H, int mode);
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode);
 long long bc_lstm_workspace_floats(int B, int H, int T);
 int bc_lstm_status(int reset);
+
+/* Diagnostic (not on the codec path; bench.py's roofline): nwg workgroups of 4 waves, each wave
+ * issuing 16 * iters v_mfma_f32_16x16x32_bf16 on random register operands (16384 FLOP each); out:
+ * nwg * 4 device floats.  Timed by the caller, it gives the dense-BF16 rate the device sustains
+ * under its clock management, the practical ceiling beside the spec peak. */
+int bc_mfma_probe(float* out, int nwg, int iters, void* stream);
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
