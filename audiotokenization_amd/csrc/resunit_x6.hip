@@ -11,7 +11,10 @@
 //            tile Hs[plane][32-ch chunk][col][32 ch] (64-B rows, 16-B groups XOR-swizzled by col so
 //            the 16 columns of a ds_read_b128 quarter-wave hit disjoint banks) - h never leaves LDS;
 //   phase 2: the k=1 conv over Hs (input as the MFMA A operand: transposed tile for the shared
-//            16-byte epilogue, conv_epilogue.h).
+//            16-byte epilogue, conv_epilogue.h).  Each wave owns one m-tile and a group of n-tiles and
+//            holds that m-tile's k=1 weights in registers (C <= 128: at most 48 VGPRs), so phase 2
+//            needs no weight copies and no barrier, and Hs may reuse the whole phase-1 LDS
+//            (Bs + As): a 96 x 128 tile fits in 80 KiB, i.e. two workgroups per CU.
 // Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
 #include "bc_common.h"
 #include "bc_internal.h"
@@ -37,14 +40,20 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;
   constexpr int CI = (BN + 6 * RU_MAX_DIL + 31) / 32;  // 32-column B passes: ncol <= BN + 6 * d
+  // phase 2 (k=1 conv): QA m-tiles x NTT n-tiles over the 8 waves, NPW n-tile groups per m-tile
+  constexpr int NTT = NT * WN;
+  static_assert(QA <= 8, "one m-tile per wave in phase 2");
+  constexpr int NPW = (8 / QA < NTT) ? 8 / QA : NTT;
+  constexpr int NTW = NTT / NPW;
+  static_assert(NTT % NPW == 0, "n-tile groups");
+  constexpr int KC1 = (16 * QA + X6_BKC - 1) / X6_BKC;  // k=1 input chunks (C = 16 * QA)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
 
   const int ncol = a.win;
   const int bplane = a.bstage;
-  const int r1 = 3 * (bplane > r.hplane ? bplane : r.hplane);
-  unsigned char* Bs = smem_ru;            // phase 1: [3][ncol][80 B]
-  unsigned char* Hs = smem_ru;            // phase 2: [3][nck1][BN][64 B] (aliases Bs)
-  unsigned char* As = smem_ru + r1;       // both phases: [2][3][QA][1 KiB]
+  unsigned char* Bs = smem_ru;                 // phase 1: [3][ncol][80 B]
+  unsigned char* As = smem_ru + 3 * bplane;    // phase 1: [2][3][QA][1 KiB]
+  unsigned char* Hs = smem_ru;                 // phase 2: [3][nck1][BN][64 B] (aliases Bs and As)
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int nt_idx = wg % a.ntn;
@@ -124,6 +133,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+
   for (int c = 0; c < a.nchunks; ++c) {
     for (int tap = 0; tap < K; ++tap) {
       const int step = c * K + tap;
@@ -168,7 +178,20 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   }
 
   // ---------------- bridge: snake2(h + b7) -> 3 bf16 planes in LDS ----------------
-  issue_a(r.w1, 0, 0);  // the k=1 conv's first weight chunk (As is free after the last barrier)
+  // this wave's phase-2 k=1 weight fragments (packed [chunk][plane][m-tile][lane][8]), loaded into
+  // registers here so they land while the bridge runs
+  const bool p2 = wave < QA * NPW;
+  const int mq = wave % QA, jg = wave / QA;
+  bf16x8_t w1f[KC1][3];
+#pragma unroll
+  for (int kc = 0; kc < KC1; ++kc)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      w1f[kc][p] = (p2 && kc < r.nck1)
+                       ? *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const unsigned char*>(r.w1) +
+                                                            ((kc * 3 + p) * QA + mq) * 1024 + lane * 16)
+                       : bf16x8_t{};
+  // (Hs overwrites Bs and As: every wave has passed the last step's barrier, no copy is in flight)
   const int C = a.Cout;
   if (C < r.nck1 * X6_BKC) {  // zero the pad channels of the last chunk (never written below)
     const int g0 = (C % X6_BKC) / 8;
@@ -210,77 +233,78 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       *reinterpret_cast<u32x2_t*>(dst + 2 * r.hplane) = (u32x2_t){l0, l1};
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
 
   // ---------------- phase 2: y = conv1(h_act), input as the MFMA A operand ----------------
+  // Wave (mq, jg) computes m-tile mq for n-tiles [jg * NTW, (jg + 1) * NTW) from its register-resident
+  // k=1 weights; Hs is read-only here, so phase 2 runs without a barrier.
+  if (p2) {
+    floatx4 acc2[1][NTW];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int j = 0; j < NTW; ++j) acc2[0][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; kc < r.nck1; ++kc) {
-    if (kc + 1 < r.nck1) issue_a(r.w1, kc + 1, (kc + 1) & 1);
-    const unsigned char* Ab = As + (kc & 1) * (a_pieces * 1024);
-    bf16x8_t bf[NT][3];
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (jg * NTW + j) * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = wn * NT * 16 + j * 16 + (lane & 15);
-      const unsigned char* src = Hs + kc * (BN * 64) + hs_off(n, lane >> 4);
+      for (int kc = 0; kc < KC1; ++kc) {
+        if (kc >= r.nck1) break;
+        const unsigned char* src = Hs + kc * (BN * 64) + hs_off(n, lane >> 4);
+        bf16x8_t bf[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bf[j][p] = *reinterpret_cast<const bf16x8_t*>(src + p * r.hplane);
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
-      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
-      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
-      const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        floatx4 t = acc[i][j];
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][2], a0, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
-        acc[i][j] = t;
+        for (int p = 0; p < 3; ++p) bf[p] = *reinterpret_cast<const bf16x8_t*>(src + p * r.hplane);
+        floatx4 t = acc2[0][j];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1], w1f[kc][1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[2], w1f[kc][0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1], w1f[kc][0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][0], t, 0, 0, 0);
+        acc2[0][j] = t;
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
+    conv_epilogue<1, NTW>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane);
   }
-
-  conv_epilogue<MT, NT>(e, acc, b, wm * MT * 16, n0 + wn * NT * 16, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-// Candidate x6 tiles (cfg ids of conv1d_x6.hip) with one m-group covering C.  Only configurations
+// Candidate x6 tiles (cfg ids of conv1d_x6.hip) with one m-group covering C, in order of preference
+// (96 x 128 first: the tile the standalone k=7 conv runs fastest at C = 96).  Only configurations
 // with <= 80 KB of LDS (two workgroups per CU, NT = 1 so 128 VGPRs suffice) are used: measured on
 // MI355X, the one-launch unit only beats the two separate convs when a second workgroup's MFMAs hide
 // each workgroup's operand loads and epilogue stores (at one workgroup per CU it was a wash at C = 48
 // and 96 and 8% slower at C = 192, profiles/r01_x6b_layer_profile.txt vs r01_resunit_v1_layers.txt).
-static const int kRUCandidates[] = {111, 110, 116, 112, 113};
+static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105};
 constexpr size_t RU_LDS_MAX = 80 * 1024;
+// BC_RU_CFG forces one candidate tile (timing experiments; it must fit the 160 KiB of a CU).
+static int ru_forced_cfg() {
+  static const int v = [] {
+    const char* e = getenv("BC_RU_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 static size_t ru_lds(const X6Tile& t, int C, int d, int* bplane, int* hplane) {
   const int ncol = x6_ncol(t, 7, 1, d);
   *bplane = (ncol * X6_PITCH + 15) / 16 * 16;
   *hplane = (C + X6_BKC - 1) / X6_BKC * x6_BN(t) * 64;
-  const int r1 = 3 * (*bplane > *hplane ? *bplane : *hplane);
-  return (size_t)r1 + 2 * 3 * (size_t)t.WM * t.MT * 1024;
+  const size_t ph1 = 3 * (size_t)*bplane + 2 * 3 * (size_t)t.WM * t.MT * 1024;  // Bs + As
+  const size_t ph2 = 3 * (size_t)*hplane;                                         // Hs
+  return ph1 > ph2 ? ph1 : ph2;
 }
 
 int resunit_select_cfg(int C, int d, int mode) {
   if (mode != 1 || C < 16 || C % 16 || d <= 0) return -1;
+  const int forced = ru_forced_cfg();
   for (int cfg : kRUCandidates) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
     if (d > RU_MAX_DIL) return -1;
     int bp, hp;
-    if (ru_lds(t, C, d, &bp, &hp) > RU_LDS_MAX) continue;
+    const size_t lds = ru_lds(t, C, d, &bp, &hp);
+    if (forced ? (cfg != forced || lds > 160 * 1024) : lds > RU_LDS_MAX) continue;
     return cfg;
   }
   return -1;
@@ -330,6 +354,11 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
     case 116: return launch_ru<3, 1, 2, 4>(a, e, r, B, st);
     case 112: return launch_ru<2, 1, 1, 8>(a, e, r, B, st);
     case 113: return launch_ru<1, 1, 1, 8>(a, e, r, B, st);
+    case 109: return launch_ru<6, 1, 1, 8>(a, e, r, B, st);
+    case 106: return launch_ru<3, 2, 1, 8>(a, e, r, B, st);
+    case 104: return launch_ru<6, 2, 1, 8>(a, e, r, B, st);
+    case 105: return launch_ru<4, 2, 1, 8>(a, e, r, B, st);
+    case 117: return launch_ru<4, 1, 2, 4>(a, e, r, B, st);
   }
   return BC_ERR_ARG;
 }
