@@ -182,9 +182,9 @@ def conv_kernel_name(cfg: int, taps: int = 0) -> str:
     if cfg >= 1000:  # phase-decomposed strided convs run the same kernels with ceil(K/s) taps
         taps = -(-taps // (cfg // 1000))
         cfg %= 1000
-    if cfg in X6_CFGS or cfg - 100 in X6_CFGS:
-        planes = 3 if cfg in X6_CFGS else 1
-        mt, nt, wm, wn = X6_CFGS[cfg if planes == 3 else cfg - 100]
+    if 100 <= cfg < 400 and cfg % 100 + 100 in X6_CFGS:
+        planes = {1: 3, 2: 1, 3: 2}[cfg // 100]
+        mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
         return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, {'true' if taps == 1 else 'false'}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
@@ -198,7 +198,9 @@ def resunit_kernel_name(cfg: int) -> str:
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6",
 # the default: same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
 # 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the LSTM stays fp32-accurate).
-PRECISIONS = {"fp32": 0, "x6": 1, "bf16": 2}
+# 3 = "h3": two fp16 planes per operand with power-of-two block scaling, three products (fp32-class
+# accuracy) at half the x6 MFMA count.
+PRECISIONS = {"fp32": 0, "x6": 1, "bf16": 2, "h3": 3}
 _mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "x6")]
 
 

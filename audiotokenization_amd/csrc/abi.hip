@@ -13,7 +13,7 @@ int bc_abi_version(void) { return BC_ABI_VERSION; }
 
 int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode) {
   if (Cout <= 0 || Cin <= 0 || K <= 0 || stride <= 0 || dilation <= 0) return -1;
-  if (mode < 0 || mode > 2) return -1;
+  if (mode < 0 || mode > 3) return -1;
   return conv_select_cfg(Cout, Cin, K, stride, dilation, mode);
 }
 
@@ -143,11 +143,12 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
 }
 
 // The recurrence is accuracy-critical: mode 2 (bf16 conv products) keeps the LSTM fp32-accurate.
+// Mode 3 (h3) runs the input projection as an h3 conv and the recurrence on the x6 persistent kernel.
 static int lstm_mode(int mode) { return mode == 2 ? 1 : mode; }
-static bool lstm_use_seq(int H, int mode) { return lstm_mode(mode) == 1 && lstm_seq_ok(H); }
+static bool lstm_use_seq(int H, int mode) { return (lstm_mode(mode) == 1 || mode == 3) && lstm_seq_ok(H); }
 
 long long bc_lstm_hh_packed_floats(int H, int mode) {
-  if (H <= 0 || H % 16 || mode < 0 || mode > 2) return -1;
+  if (H <= 0 || H % 16 || mode < 0 || mode > 3) return -1;
   if (lstm_use_seq(H, mode)) return lstm_seq_packed_bytes(H) / 4;
   return (long long)4 * H * H;
 }
@@ -157,7 +158,7 @@ int bc_lstm_status(int reset) { return lstm_seq_read_status(reset); }
 int bc_mfma_probe(float* out, int nwg, int iters, void* stream) { return mfma_probe_launch(out, nwg, iters, S(stream)); }
 
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode) {
-  if (!w_hh_host || !packed_host || H <= 0 || H % 16 || mode < 0 || mode > 2) return BC_ERR_ARG;
+  if (!w_hh_host || !packed_host || H <= 0 || H % 16 || mode < 0 || mode > 3) return BC_ERR_ARG;
   if (lstm_use_seq(H, mode))
     lstm_seq_pack(w_hh_host, reinterpret_cast<unsigned short*>(packed_host), H);  // persistent kernel
   else if (lstm_fast_ok(H))
@@ -183,7 +184,7 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
                    const float* out_snake_inv_beta, float* workspace, int mode, void* stream) {
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
-      H % 16 || T < 0 || num_layers <= 0 || mode < 0 || mode > 2)
+      H % 16 || T < 0 || num_layers <= 0 || mode < 0 || mode > 3)
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;

@@ -203,8 +203,8 @@ static Geometry geometry(const Tile& t, int bkc, int K, int s, int d) {
 }
 
 int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode) {
-  if (mode == 1 || mode == 2) {
-    const int c = x6_select_cfg(Cout, Cin, K, stride, dilation, mode == 1 ? 3 : 1);
+  if (mode >= 1 && mode <= 3) {
+    const int c = x6_select_cfg(Cout, Cin, K, stride, dilation, mode == 1 ? 3 : mode == 2 ? 1 : 2);
     if (c >= 0) return c;
   }
   int tile;

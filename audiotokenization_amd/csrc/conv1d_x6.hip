@@ -18,6 +18,8 @@
 //                channel-contiguous ([col][32 ch], 80-B pitch: conflict-free b128 reads at stride 1)
 //                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
 //                at tap 0 and land while the current chunk's taps compute.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -28,8 +30,13 @@
 
 namespace bc {
 
-// P = operand planes: 3 (x6, fp32-accurate) or 1 (plain bf16 products: the "bf16" precision mode of
-// BASELINE config 5, activations still stored fp32).
+// P = operand planes: 3 (x6, fp32-accurate), 2 ("h3": two fp16 planes, three products, fp32-class
+// accuracy at half the x6 MFMA count, x6_common.h) or 1 (plain bf16 products: the "bf16" precision
+// mode of BASELINE config 5, activations still stored fp32).
+// h3 scaling: each staged 32-channel B chunk gets a power-of-two scale from its block maximum (a wave
+// reduction + an LDS exchange folded into the barrier in front of the chunk's store); the scale only
+// ever decreases within a workgroup, the accumulator is rescaled (exactly) when it does, and the
+// epilogue multiplies by 1 / (x scale * per-row weight scale).
 // PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
 template <int MT, int NT, int WM, int WN, int P, bool PW>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
@@ -40,6 +47,8 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
   constexpr int CI = PW ? BN / 32 : X6_MAXCOL_ITERS;  // 32-column B passes per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
+  __shared__ unsigned smax[2][8];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
+  typedef typename FragType<P>::type frag_t;
 
   const int ncol = a.win;                // columns of the input tile
   const int bplane = a.bstage;           // bytes per B plane (multiple of 16)
@@ -110,12 +119,39 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       v1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
     }
   };
+  // P == 2: publish this wave's block maximum of a chunk's staged values / read the block's scale
+  auto bmax_publish = [&](const float (&w0)[CI], const float (&w1)[CI], int par) {
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < CI; ++i) {
+      const unsigned u0 = __float_as_uint(fabsf(w0[i])), u1 = __float_as_uint(fabsf(w1[i]));
+      m = m > u0 ? m : u0;
+      m = m > u1 ? m : u1;
+    }
+    m = wave_max_u32(m);
+    if (lane == 0) smax[par][wave] = m;
+  };
+  auto bmax_scale = [&](int par) {
+    unsigned m = smax[par][0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = m > smax[par][w] ? m : smax[par][w];
+    return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
+  };
+  float xs = 1.f;  // P == 2: scale of the staged chunk and of the accumulator
   auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI]) {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       if (col < ncol) {
         const float v0 = w0[i], v1 = w1[i];
+        if constexpr (P == 2) {
+          unsigned h, m;
+          split2_h(v0 * xs, v1 * xs, h, m);
+          unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+          *reinterpret_cast<unsigned*>(p) = h;
+          *reinterpret_cast<unsigned*>(p + bplane) = m;
+          continue;
+        }
         const unsigned h = pk_bf16(v0, v1);
         unsigned char* p = Bs + col * X6_PITCH + bp * 4;
         *reinterpret_cast<unsigned*>(p) = h;
@@ -137,6 +173,20 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // P == 2, at a chunk boundary (the previous chunk's B tile is no longer read): the next chunk's
+  // scale = min(current, its block scale); the accumulator follows exactly (powers of two)
+  auto h3_next_scale = [&](int par) {
+    const float sn = bmax_scale(par);
+    if (sn < xs) {
+      const float r = sn / xs;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] *= r;
+      xs = sn;
+    }
+  };
+
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
   const int kgrp16 = (lane >> 4) * 16;
 
@@ -144,16 +194,28 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   auto compute = [&](int step, int tap) {
       const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
       const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
-      bf16x8_t bf[NT][P];
+      frag_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          bf[j][p] = *reinterpret_cast<const bf16x8_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
+          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
-        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+        const frag_t a0 = *reinterpret_cast<const frag_t*>(Aq);
+        if constexpr (P == 2) {
+          const frag_t a1 = *reinterpret_cast<const frag_t*>(Aq + QA * 1024);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            floatx4 t = acc[i][j];
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][1], a0, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a1, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a0, t, 0, 0, 0);
+            acc[i][j] = t;
+          }
+          continue;
+        } else {
         if (P == 1) {
 #pragma unroll
           for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
@@ -173,12 +235,18 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
           acc[i][j] = t;
         }
+        }
       }
   };
 
   // prologue: A(step 0), B(chunk 0)
   issue_a(0, 0);
   load_b(0, bv0, bv1);
+  if constexpr (P == 2) {
+    bmax_publish(bv0, bv1, 0);
+    lds_barrier();
+    xs = bmax_scale(0);
+  }
   store_b(bv0, bv1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -193,7 +261,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       if (c + 2 < a.nchunks && !(a.dbg & 2)) load_b(c + 2, p0v, p1v);
       compute(c, 0);
       if (c + 1 < a.nchunks) {
+        if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
+        if constexpr (P == 2) h3_next_scale((c + 1) & 1);
         if (!(a.dbg & 4)) store_b(n0v, n1v);
       }
       // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
@@ -215,7 +285,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
         if (tap == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
         compute(step, tap);
         if (tap == K - 1 && c + 1 < a.nchunks) {
+          if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
+          if constexpr (P == 2) h3_next_scale((c + 1) & 1);
           if (!(a.dbg & 4)) store_b(bv0, bv1);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
@@ -231,7 +303,12 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     }
   }
 
-  if (!(a.dbg & 8)) conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
+  if (!(a.dbg & 8)) {
+    if constexpr (P == 2)
+      conv_epilogue<MT, NT, true>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
+    else
+      conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -265,7 +342,8 @@ static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
   return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
 }
 
-// cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane); + 1000 * s for a stride-s
+// cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane), 300 + tile (h3, two fp16
+// planes); + 1000 * s for a stride-s
 // conv run by phase decomposition (ConvArgs::ps): the stride-1 conv with ceil(K/s) taps over s * Cin
 // phase channels ci' = ci * s + r, weights W'[co][ci'][q] = W[co][ci][q * s + r] (0 past K).  Its
 // input tile needs BN + ceil(K/s) - 1 columns instead of (BN - 1) * s + K, so the wide 128 x 256
@@ -274,13 +352,16 @@ static inline int cfg_base(int cfg) { return cfg % 1000; }
 static inline int cfg_phase(int cfg) { return cfg / 1000; }
 bool x6_cfg_valid(int cfg) {
   const int b = cfg_base(cfg), s = cfg_phase(cfg);
-  return ((b >= 100 && b < 100 + X6_NT) || (b >= 200 && b < 200 + X6_NT)) && (s == 0 || (s >= 2 && s <= 16));
+  return ((b >= 100 && b < 100 + X6_NT) || (b >= 200 && b < 200 + X6_NT) || (b >= 300 && b < 300 + X6_NT)) &&
+         (s == 0 || (s >= 2 && s <= 16));
 }
-static inline int cfg_planes(int cfg) { return cfg_base(cfg) >= 200 ? 1 : 3; }
-static inline const X6Tile& cfg_tile(int cfg) {
+// 100..: x6 (3 bf16 planes), 200..: bf16 (1 plane), 300..: h3 (2 fp16 planes + per-row scales)
+static inline int cfg_planes(int cfg) {
   const int b = cfg_base(cfg);
-  return kX6Tiles[b >= 200 ? b - 200 : b - 100];
+  return b >= 300 ? 2 : b >= 200 ? 1 : 3;
 }
+static inline int planes_base(int planes) { return planes == 1 ? 200 : planes == 2 ? 300 : 100; }
+static inline const X6Tile& cfg_tile(int cfg) { return kX6Tiles[cfg_base(cfg) % 100]; }
 const X6Tile& x6_tile(int cfg) { return cfg_tile(cfg); }
 
 // Returns a x6 (planes = 3) / bf16 (planes = 1) cfg id, or -1 when the shape should stay on the
@@ -339,9 +420,9 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
-  if (planes == 3 && x6_occ_pref() == 0) {
+  if (planes >= 2 && x6_occ_pref() == 0) {
     const int c = x6_preferred_cfg(Cout, Cin, K, s, d);
-    if (c >= 0) return c;
+    if (c >= 0) return c + (planes == 2 ? 200 : 0);
   }
   if (x6_phase_ok(s, d)) {
     const int c = x6_select_tile(Cout, Cin * s, (K + s - 1) / s, 1, 1, planes);
@@ -389,7 +470,7 @@ static int x6_select_tile(int Cout, int Cin, int K, int s, int d, int planes) {
     const int ncol = x6_ncol(t, K, s, d);
     if (ncol > 32 * X6_MAXCOL_ITERS) continue;
     if (x6_lds(t, ncol, planes) > (occ4[i] ? 80 : 160) * 1024) continue;
-    return (planes == 1 ? 200 : 100) + order[i];
+    return planes_base(planes) + order[i];
   }
   return -1;
 }
@@ -402,7 +483,8 @@ long long x6_packed_bytes(int Cout, int Cin, int K, int cfg) {
   }
   const int ntm = (Cout + x6_BM(t) - 1) / x6_BM(t);
   const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
-  return (long long)ntm * nchunks * K * cfg_planes(cfg) * t.WM * t.MT * 1024;
+  const long long planes = (long long)ntm * nchunks * K * cfg_planes(cfg) * t.WM * t.MT * 1024;
+  return planes + (cfg_planes(cfg) == 2 ? (long long)ntm * x6_BM(t) * 4 : 0);  // h3: + 1 / row scale
 }
 
 static inline unsigned short f2bf_rn(float f) {
@@ -411,6 +493,17 @@ static inline unsigned short f2bf_rn(float f) {
   if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);  // NaN
   const unsigned r = u + 0x7fffu + ((u >> 16) & 1u);
   return (unsigned short)(r >> 16);
+}
+static inline unsigned short f2h_rn(float f) {
+  const _Float16 h = (_Float16)f;  // IEEE round-to-nearest-even
+  unsigned short u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+static inline float h2f(unsigned short u) {
+  _Float16 h;
+  memcpy(&h, &u, 2);
+  return (float)h;
 }
 static inline float bf2f(unsigned short h) {
   const unsigned u = (unsigned)h << 16;
@@ -436,6 +529,16 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
   const int BM = x6_BM(t), QA = t.WM * t.MT;
   const int ntm = (Cout + BM - 1) / BM;
   const int nchunks = (Cin + X6_BKC - 1) / X6_BKC;
+  // h3: per-row power-of-two scale 2^(14 - e), 2^e <= max |w[row]| < 2^(e+1) (see x6_common.h)
+  std::vector<float> rsc(P == 2 ? (size_t)ntm * BM : 0, 1.f);
+  for (size_t row = 0; row < rsc.size() && (int)row < Cout; ++row) {
+    float m = 0.f;
+    for (long long k = 0; k < (long long)Cin * K; ++k) m = std::max(m, std::fabs(w[(long long)row * Cin * K + k]));
+    if (m > 0.f && std::isfinite(m)) {
+      const int e = std::max(-112, std::min(140, std::ilogb(m)));
+      rsc[row] = std::ldexp(1.f, 14 - e);
+    }
+  }
   long long o = 0;
   for (int mg = 0; mg < ntm; ++mg)
     for (int c = 0; c < nchunks; ++c)
@@ -448,6 +551,12 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
                 const int ci = c * X6_BKC + 8 * (lane >> 4) + j;
                 float v = 0.f;
                 if (row < Cout && ci < Cin) v = w[((long long)row * Cin + ci) * K + tap];
+                if (P == 2) {
+                  const float vs = v * rsc[row];
+                  const unsigned short g0 = f2h_rn(vs);
+                  out[o] = p == 0 ? g0 : f2h_rn(vs - h2f(g0));
+                  continue;
+                }
                 const unsigned short h0 = f2bf_rn(v);
                 const float r1 = v - bf2f(h0);
                 const unsigned short h1 = f2bf_rn(r1);
@@ -455,6 +564,10 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
                 const unsigned short h2 = f2bf_rn(r2);
                 out[o] = p == 0 ? h0 : p == 1 ? h1 : h2;
               }
+  if (P == 2) {  // 1 / row scale after the planes (ConvArgs::wsc)
+    float* inv = reinterpret_cast<float*>(out + o);
+    for (size_t row = 0; row < rsc.size(); ++row) inv[row] = 1.f / rsc[row];
+  }
 }
 
 // BC_X6_PW=0 runs pointwise convs on the general kernel (A/B timing).
@@ -482,6 +595,9 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
   if ((long long)(a.ps ? a.cin0 : a.Cin) * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
+  a.wsc = P == 2 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
+                                                  (long long)a.ntm * a.nchunks * a.K * P * t.WM * t.MT * 1024)
+                 : nullptr;
   const size_t lds = x6_lds(t, ncol, P);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   if (a.K == 1 && ncol == BN && x6_pw_on())
@@ -510,7 +626,8 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
   }
 #define BC_X6_CASES(ID, MT, NT, WM, WN)                                \
   case 100 + ID: return launch_x6<MT, NT, WM, WN, 3>(a, B, st);        \
-  case 200 + ID: return launch_x6<MT, NT, WM, WN, 1>(a, B, st);
+  case 200 + ID: return launch_x6<MT, NT, WM, WN, 1>(a, B, st);        \
+  case 300 + ID: return launch_x6<MT, NT, WM, WN, 2>(a, B, st);
   switch (cfg) {
     BC_X6_CASES(0, 4, 4, 2, 4)
     BC_X6_CASES(1, 4, 2, 2, 4)

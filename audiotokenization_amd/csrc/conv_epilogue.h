@@ -24,9 +24,11 @@ __device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, fl
 
 // acc[i][j]: transposed 16x16 tiles; rows (channels) start at row0 + 16 i, columns (positions) at
 // col0 + 16 j.
-template <int MT, int NT>
+// SC (h3 kernels): the accumulator holds x*S_x times w*S_w[co] products; acc * (a.wsc[co] * xinv)
+// (a power of two: exact) restores the fp32 dot product before the bias is added.
+template <int MT, int NT, bool SC = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
-                                              int col0, int lane) {
+                                              int col0, int lane, float xinv = 1.f) {
   float* yb = a.y + (long long)b * a.ybs;
   float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
@@ -38,6 +40,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
     const float bias = a.bias ? a.bias[co] : 0.f;
     const float sa = snk ? a.osa[co] : 0.f;
     const float sb = snk ? a.osb[co] : 0.f;
+    const float sc = SC ? a.wsc[co] * xinv : 1.f;
     const long long rowoff = (long long)co * a.yT + a.ooff;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -49,7 +52,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
         if (rb) r = *reinterpret_cast<const floatx4*>(rb + yi);
         floatx4 v, sv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = conv_epi_value(a, acc[i][j][q], bias, r[q], rb != nullptr);
+        for (int q = 0; q < 4; ++q)
+          v[q] = conv_epi_value(a, SC ? acc[i][j][q] * sc : acc[i][j][q], bias, r[q], rb != nullptr);
         if (snk) {
           const f32x2 lo = snake_pk((f32x2){v[0], v[1]}, splat2(sa), splat2(sb));
           const f32x2 hi = snake_pk((f32x2){v[2], v[3]}, splat2(sa), splat2(sb));
@@ -69,7 +73,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
           const int n = nb + q;
           if (n >= a.Nout) break;
           const long long yi = rowoff + (long long)n * a.ostride;
-          const float v = conv_epi_value(a, acc[i][j][q], bias, rb ? rb[yi] : 0.f, rb != nullptr);
+          const float v =
+              conv_epi_value(a, SC ? acc[i][j][q] * sc : acc[i][j][q], bias, rb ? rb[yi] : 0.f, rb != nullptr);
           if (snk) {
             const float sv = snake(v, sa, sb);
             if (y2b) {

@@ -13,6 +13,8 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 
 constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
 constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
@@ -40,6 +42,50 @@ __device__ __forceinline__ void split2(float v0, float v1, unsigned& h, unsigned
   const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
   l = pk_bf16(s0, s1);
 }
+
+// ---- "h3" operands (precision mode 3): two fp16 planes per fp32 value, three products ----
+// v*S = h + m with h = fp16_rn(v*S), m = fp16_rn(v*S - h) (the residual v*S - h is exact in fp32), so
+// |v*S - h - m| <= 2^-22 |v*S|; a*b is accumulated as a0b0 + a0b1 + a1b0 (a1b1 <= 2^-22 |ab| dropped).
+// fp16 has 11 significant bits (3 more than bf16) but a 5-bit exponent, so every operand block is
+// scaled by a power of two S = 2^(14 - e) with 2^e <= amax < 2^(e+1): |v*S| < 2^15 < 65504, and an
+// element far below amax only loses precision that is negligible against amax (the dot-product
+// scale): its absolute error stays below 2^-25 / S = 2^-39 amax.  Scaling by 2^k is exact, so the
+// fp32 MFMA accumulation of the scaled products is the scaled accumulation of the unscaled ones.
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+  const f16x2_t v = __builtin_convertvector((float2_t){a, b}, f16x2_t);
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float f16_lo(unsigned p) {
+  return (float)__builtin_bit_cast(f16x2_t, p)[0];
+}
+__device__ __forceinline__ float f16_hi(unsigned p) {
+  return (float)__builtin_bit_cast(f16x2_t, p)[1];
+}
+// split of two (already scaled) fp32 values into two packed fp16x2 planes
+__device__ __forceinline__ void split2_h(float v0, float v1, unsigned& h, unsigned& m) {
+  h = pk_f16(v0, v1);
+  m = pk_f16(v0 - f16_lo(h), v1 - f16_hi(h));
+}
+// exponent e of a block maximum (bits of a non-negative float) -> scale 2^(14 - e), clamped to a
+// normal fp32; an all-zero block gets 1
+__device__ __forceinline__ float h3_scale_from_bits(unsigned amax_bits) {
+  int e = (int)(amax_bits >> 23) - 127;
+  if (amax_bits == 0) e = 14;
+  e = e < -112 ? -112 : (e > 140 ? 140 : e);
+  return __uint_as_float((unsigned)(127 + 14 - e) << 23);
+}
+// max over the 64 lanes of a wave (non-negative float bits compare as unsigned ints)
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned w = (unsigned)__shfl_xor((int)v, o, 64);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+
+template <int P> struct FragType { typedef bf16x8_t type; };
+template <> struct FragType<2> { typedef f16x8_t type; };
 
 // host-side tile geometry
 struct X6Tile {

@@ -36,6 +36,7 @@ METRIC = "audio-sec encoded/sec/GPU (24 kHz mono, 10 s clips) + VQ index bit-exa
 METRIC_RT = "audio-sec encoded+quantised+decoded/sec (24 kHz mono, 10 s clips)"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec); 155 measured
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
+H3_PRODUCTS = 3  # csrc/conv1d_x6.hip P = 2: three fp16 MFMAs per product term
 X6_PRODUCTS = 6  # csrc/conv1d_x6.hip: six bf16 MFMAs per fp32-accurate product term
 HBM_PEAK_GBS = 8000.0
 
@@ -53,6 +54,10 @@ def kernel_peak(kname: str):
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
     if kname.startswith("conv1d_x6_kernel") and len(targs) >= 5 and targs[4] == "1":  # P = 1 plane
         return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"
+    if kname.startswith("conv1d_x6_kernel") and len(targs) >= 5 and targs[4] == "2":  # h3: 2 fp16 planes
+        return (BF16_MFMA_PEAK_TFLOPS / H3_PRODUCTS, H3_PRODUCTS,
+                "2xfp16 split (h3): every fp32 multiply-add costs 3 fp16 MFMA multiply-adds (dense FP16 MFMA peak "
+                "= BF16's), so the fp32-equivalent ceiling is the dense FP16 MFMA peak / 3")
     if kname.startswith("conv1d_x6_kernel"):
         return (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS, X6_PRODUCTS,
                 "3xbf16 split: every fp32 multiply-add costs 6 bf16 MFMA multiply-adds, so the fp32-equivalent "
@@ -73,7 +78,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true")
     p.add_argument("--cpu-clips", type=int, default=1)
-    p.add_argument("--precision", choices=["fp32", "x6", "bf16"], default=None,
+    p.add_argument("--precision", choices=["fp32", "x6", "bf16", "h3"], default=None,
                    help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or x6)")
     a = p.parse_args()
     c = CONFIGS[a.config]
@@ -295,6 +300,7 @@ def main():
             parity["note"] = "waveforms compared end to end; equal codes make it the decoder's error alone"
     if rank == 0:
         dtype = {"fp32": "f32", "x6": "f32 (3xbf16-split MFMA, fp32 accumulate)",
+                 "h3": "f32 (2xfp16 block-scaled split MFMA, fp32 accumulate)",
                  "bf16": "bf16 conv products, fp32 accumulate/storage (LSTM and VQ fp32-accurate)"}[args.precision]
         if cfgn == 4 and state["host"] is not None:
             assert state["host"].dtype == np.int16

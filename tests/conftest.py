@@ -38,10 +38,10 @@ def golden():
     return load_golden
 
 
-@pytest.fixture(params=["fp32", "x6"])
+@pytest.fixture(params=["fp32", "x6", "h3"])
 def prec(request):
-    """Run a test under both conv GEMM precisions: native fp32 MFMA and the fp32-accurate 3xbf16
-    split MFMA (csrc/conv1d_x6.hip)."""
+    """Run a test under every fp32-class conv GEMM precision: native fp32 MFMA, the 3xbf16 split MFMA
+    ("x6") and the 2xfp16 block-scaled split MFMA ("h3"), csrc/conv1d_x6.hip."""
     from audiotokenization_amd import _lib
 
     old = _lib.precision_mode()

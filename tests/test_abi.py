@@ -138,7 +138,7 @@ def test_lstm_seq_pack_layout(H):
 def test_bad_arguments_are_rejected_without_launching():
     lib = L.load()
     assert lib.bc_conv1d_select_cfg(0, 4, 7, 1, 1, 0) == -1
-    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 3) == -1  # unknown precision mode
+    assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 4) == -1  # unknown precision mode
     assert lib.bc_conv1d_select_cfg(48, 48, 7, 1, 1, 2) >= 200  # bf16 products: one-plane tiles
     assert lib.bc_conv1d_select_cfg(8, 4, 7, 1, 1, 1) in L.CONV_CFGS  # x6 needs Cin >= 16: fp32 kernel
     assert lib.bc_conv1d_packed_floats(8, 8, 0, 0) == -1
@@ -147,7 +147,7 @@ def test_bad_arguments_are_rejected_without_launching():
     # dual output without an epilogue Snake, tanh together with a Snake: rejected
     assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, 1, 1, 8, 8, 8, 8, 3, 1, 1, 1, 0, 4, None) == 1
     assert lib.bc_lstm_hh_packed_floats(10, 0) == -1
-    assert lib.bc_lstm_hh_packed_floats(512, 3) == -1
+    assert lib.bc_lstm_hh_packed_floats(512, 4) == -1
     assert lib.bc_vq_prepare_codebook(1, 1, 1, 8192, 16, None) == 3
     assert lib.bc_synth_clips(None, 1, 10, 0, None) == 1
     assert lib.bc_convT1d_phase_taps(10, 5) == 2 and lib.bc_convT1d_phase_taps(1, 1) == 1
@@ -160,3 +160,41 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), f
+
+
+@pytest.mark.parametrize("Cout,Cin,K", [(48, 48, 7), (1536, 768, 10), (6144, 1536, 1), (20, 36, 5)])
+def test_h3_pack_layout_and_scaled_split(Cout, Cin, K):
+    """h3 mode (precision 3) packs each weight as two fp16 planes of w * S[row] (S = 2^(14 - e) with
+    2^e <= max|w[row]| < 2^(e+1)), h0 = fp16(w S), h1 = fp16(w S - h0), in the x6 plane order, followed
+    by 1 / S[row] for every packed row (conv1d_x6.hip, x6_common.h)."""
+    lib = L.load()
+    cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, 1, 3)
+    assert cfg % 1000 >= 300
+    mt, nt, wm, wn = L.X6_CFGS[cfg % 100 + 100]
+    bm, qa = 16 * mt * wm, mt * wm
+    ntm, nch = -(-Cout // bm), -(-Cin // 32)
+    n = lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg)
+    main = ntm * nch * K * 2 * qa * 1024
+    assert n * 4 == main + ntm * bm * 4
+    rng = np.random.default_rng(2)
+    w = (rng.standard_normal((Cout, Cin, K)) * np.exp(rng.standard_normal((Cout, 1, 1)) * 6)).astype(np.float32)
+    w[0] = 0.0  # an all-zero row keeps scale 1
+    out = np.empty(n, np.float32)
+    assert lib.bc_conv1d_pack(w.ctypes.data, out.ctypes.data, Cout, Cin, K, cfg) == 0
+    P = out[: main // 4].view(np.float16).reshape(ntm, nch, K, 2, qa, 64, 8).astype(np.float64)
+    inv = out[main // 4:].astype(np.float64)
+    amax = np.abs(w).reshape(Cout, -1).max(axis=1).astype(np.float64)
+    S = np.where(amax > 0, 2.0 ** (14 - np.floor(np.log2(np.where(amax > 0, amax, 1.0)))), 1.0)
+    assert np.array_equal(inv[:Cout], 1.0 / S)
+    assert (np.abs(w).reshape(Cout, -1).max(axis=1) * S < 2.0 ** 15).all()
+    for _ in range(300):
+        mg, c, tap, q, lane, j = (int(rng.integers(s)) for s in (ntm, nch, K, qa, 64, 8))
+        row = mg * bm + q * 16 + (lane & 15)
+        ci = c * 32 + 8 * (lane >> 4) + j
+        h0, h1 = P[mg, c, tap, 0, q, lane, j], P[mg, c, tap, 1, q, lane, j]
+        if row >= Cout or ci >= Cin:
+            assert h0 == 0 and h1 == 0
+            continue
+        ws = float(w[row, ci, tap]) * S[row]
+        assert h0 == float(np.float16(ws))
+        assert abs(ws - h0 - h1) <= abs(ws) * 2.0 ** -22 + 2.0 ** -25

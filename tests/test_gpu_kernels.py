@@ -188,7 +188,8 @@ def test_reslstm(dev, H, layers, B, T, prec):
 @pytest.mark.parametrize("Cin,Cout,K,d", [(384, 384, 7, 9), (1536, 1024, 3, 1), (96, 96, 7, 1), (768, 768, 1, 1)])
 def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
     """The 3xbf16-split MFMA conv is fp32-accurate: its error against an fp64 evaluation is no larger
-    than (1.25x) the native fp32 MFMA kernel's, measured as max |y - y64| / max(sum |w x|)."""
+    than (1.25x) the native fp32 MFMA kernel's, measured as max |y - y64| / max(sum |w x|).  The
+    2xfp16 block-scaled split ("h3", 22-bit operands) stays within 2x of it."""
     g = torch.Generator().manual_seed(Cin + K)
     m = CV.WNConv1d(Cin, Cout, kernel_size=K, dilation=d, padding=K // 2 * d)
     conv = _rand_wn_conv(m, g)
@@ -201,16 +202,47 @@ def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
     errs = {}
     old = L.precision_mode()
     try:
-        for p in ("fp32", "x6"):
+        for p in ("fp32", "x6", "h3"):
             L.set_precision(p)
             y = m.run(x.to(dev)).cpu().double()
             errs[p] = float((y - y64).abs().max() / scale)
     finally:
         L._mode = old
     print(f"conv {Cin}->{Cout} k{K} d{d}: max|y - y64| / max(sum|w x|): fp32 MFMA {errs['fp32']:.3e}, "
-          f"x6 {errs['x6']:.3e}")
+          f"x6 {errs['x6']:.3e}, h3 {errs['h3']:.3e}")
     assert errs["x6"] <= 1.25 * errs["fp32"] + 1e-9, errs
+    assert errs["h3"] <= 2.0 * errs["fp32"] + 1e-9, errs
     assert errs["fp32"] < 1e-6, errs
+
+
+@pytest.mark.parametrize("Cin,K,pw", [(96, 7, False), (256, 1, True), (160, 3, False)])
+def test_h3_block_scaling(dev, Cin, K, pw):
+    """h3 block scaling: channel groups whose magnitudes span 1e-30 .. 1e30 (beyond fp16's range in
+    both directions; chunks of 32 channels that grow and shrink, so the per-chunk scale changes and the
+    accumulator is rescaled) and all-zero chunks.  Each output's error against fp64 stays at the fp32
+    level of its own |w||x| scale."""
+    g = torch.Generator().manual_seed(Cin * 3 + K)
+    Cout = 64
+    m = CV.WNConv1d(Cin, Cout, kernel_size=K, padding=K // 2)
+    conv = _rand_wn_conv(m, g)
+    mags = torch.tensor([1e-30, 1.0, 1e30, 0.0, 1e-3, 1e12, 1e-12, 7.0])
+    grp = mags[(torch.arange(Cin) // 32) % len(mags)].view(1, Cin, 1)
+    x = torch.randn(2, Cin, 260, generator=g) * grp
+    sd = {k: v.detach() for k, v in conv.state_dict().items()}
+    w = O.wn_weight(sd, "").double()
+    y64 = F.conv1d(x.double(), w, sd["bias"].double(), 1, K // 2, 1)
+    scale = F.conv1d(x.double().abs(), w.abs(), None, 1, K // 2, 1) + sd["bias"].double().abs().view(1, -1, 1)
+    m.to(dev)
+    old = L.precision_mode()
+    try:
+        L.set_precision("h3")
+        y = m.run(x.to(dev)).cpu().double()
+    finally:
+        L._mode = old
+    assert torch.isfinite(y).all()
+    rel = ((y - y64).abs() / scale).max().item()
+    print(f"h3 block scaling Cin={Cin} K={K}: max |y - y64| / (sum|w x| + |b|) = {rel:.3e}")
+    assert rel < 2e-6, rel
 
 
 @pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, False, 1, 700), (96, 3, False, 2, 513),
