@@ -191,17 +191,18 @@ def conv_kernel_name(cfg: int, taps: int = 0) -> str:
 
 
 def resunit_kernel_name(cfg: int) -> str:
-    mt, nt, wm, wn = X6_CFGS[cfg]
-    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}>"
+    mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
+    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, {2 if cfg >= 300 else 3}>"
 
 
-# Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6",
-# the default: same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
-# 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the LSTM stays fp32-accurate).
-# 3 = "h3": two fp16 planes per operand with power-of-two block scaling, three products (fp32-class
-# accuracy) at half the x6 MFMA count.
+# Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6":
+# same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
+# 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the LSTM stays fp32-accurate),
+# 3 = "h3", the default: two fp16 planes per operand with power-of-two block scaling, three products
+# (fp32-class accuracy, measured below the fp32 MFMA kernel's error) at half the x6
+# MFMA count.
 PRECISIONS = {"fp32": 0, "x6": 1, "bf16": 2, "h3": 3}
-_mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "x6")]
+_mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "h3")]
 
 
 def set_precision(name: str) -> None:

@@ -84,11 +84,12 @@ class ResidualUnit(nn.Module):
         return self.block[0]
 
     def _fused_cfg(self):
-        """cfg of the one-launch unit (bc_resunit_fwd), or -1 (x6 mode, no anti-aliasing, C fits)."""
-        if L.precision_mode() != 1 or self.block[2].antialias:
+        """cfg of the one-launch unit (bc_resunit_fwd), or -1 (x6 / h3 mode, no anti-aliasing, C fits)."""
+        mode = L.precision_mode()
+        if mode not in (1, 3) or self.block[2].antialias:
             return -1
         conv7 = _conv_of(self.block[1])
-        return L.load().bc_resunit_select_cfg(conv7.in_channels, conv7.dilation, 1)
+        return L.load().bc_resunit_select_cfg(conv7.in_channels, conv7.dilation, mode)
 
     def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
         """x_act = self.first_act(x_raw) (computed by the producer)."""

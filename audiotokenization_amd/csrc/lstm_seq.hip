@@ -27,10 +27,14 @@
 //   miss pulls the line into that XCD's L2 for the other 23.  (Measured: sc1 loads of a reused
 //   double buffer instead — every CU fetching its 393 KB over the fabric — cost 11.6 us per step.)
 //   Every poll is bounded: on timeout the kernel counts it in *status and all workgroups leave.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "bc_common.h"
 #include "bc_internal.h"
+#include "x6_common.h"
 
 namespace bc {
 
@@ -61,6 +65,9 @@ struct LstmSeqArgs {
 };
 
 constexpr int LS_STAMP_T = 2048;  // steps recorded per stamped workgroup
+
+template <int P> struct LsFrag { typedef __bf16 type __attribute__((ext_vector_type(8))); };
+template <> struct LsFrag<2> { typedef _Float16 type __attribute__((ext_vector_type(8))); };
 
 __device__ __forceinline__ unsigned ls_pk(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector((ls_float2){a, b}, ls_bf16x2));
@@ -307,8 +314,12 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
 //   hseq[t][half][k-step][n-tile (2)][plane][lane][8 bf16]; flags[half][G]; one cell per thread per
 //   half (tile p = wave: m-tile p>>1, n-tile p&1).
 // ------------------------------------------------------------------------------------------------
-template <int KS>
+// P = 3: x6 (3 bf16 planes, 6 products).  P = 2: h3 (2 fp16 planes, 3 products, x6_common.h): W_hh
+// rows are pre-scaled on the host by 2^(14 - e_row) (1 / scale stored after the planes), h_t in
+// (-1, 1) is split with the fixed scale 2^14, and the summed gate products are unscaled per gate row.
+template <int KS, int P>
 __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
+  typedef typename LsFrag<P>::type frag_t;
   constexpr int NH = 32;                       // clips per half
   __shared__ floatx4 red[LS_WAVES][4][64];     // per-wave partial gates of one half's 4 tiles
   __shared__ float hs[NH][LS_U + 1];           // one half's h_t gathered per clip
@@ -322,22 +333,29 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
   const long long TB = (long long)a.T * a.Btot;
   if (tid == 0) bail = 0;
 
-  ls_bf16x8 wr[2][KS][3];
+  frag_t wr[2][KS][P];
   {
-    const ls_bf16x8* wp = reinterpret_cast<const ls_bf16x8*>(a.whh) + (long long)(g * LS_WAVES + w) * (2 * KS * 3) * 64 + lane;
+    const frag_t* wp = reinterpret_cast<const frag_t*>(a.whh) + (long long)(g * LS_WAVES + w) * (2 * KS * P) * 64 + lane;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) wr[mt][ks][p] = wp[((mt * KS + ks) * 3 + p) * 64];
+        for (int p = 0; p < P; ++p) wr[mt][ks][p] = wp[((mt * KS + ks) * P + p) * 64];
   }
 
   const int cu = (w >> 1) * 4 + (lane >> 4);   // my cell's unit within the workgroup
+  // P == 2: 1 / (row scale * h scale 2^14) of my cell's four gate rows
+  float gsc[4] = {1.f, 1.f, 1.f, 1.f};
+  if constexpr (P == 2) {
+    const float* wsc = reinterpret_cast<const float*>(a.whh + (long long)4 * H * H * P);
+#pragma unroll
+    for (int gate = 0; gate < 4; ++gate) gsc[gate] = wsc[gate * H + g * LS_U + cu] * (1.0f / 16384.0f);
+  }
   const int cbh = (w & 1) * 16 + (lane & 15);  // my cell's clip within a half
   float cst0 = 0.f, cst1 = 0.f;                // my cell's c in half 0 / half 1
 
-  const long long hhalf = (long long)H * (LS_HSTEP_PER_UNIT / 2);  // floats of hseq per half-step
+  const long long hhalf = (long long)H * (LS_NB * P / 2 / 2);  // floats of hseq per half-step
   const int nprod = G / LS_WAVES;
   ls_gu32* flags = (ls_gu32*)(a.flags);
   int pend_h = -1;        // wave 0: half whose h stores are issued but whose flag is not yet set
@@ -384,15 +402,15 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         LS2_STAMP(1)
-        const ls_bf16x8* hp =
-            reinterpret_cast<const ls_bf16x8*>(a.hseq + ((long long)(t - 1) * 2 + h) * hhalf) + lane;
-        ls_bf16x8 hbuf[2][2][3];
-        auto load_ks = [&](int ks, ls_bf16x8 (&dst)[2][3]) {
+        const frag_t* hp =
+            reinterpret_cast<const frag_t*>(a.hseq + ((long long)(t - 1) * 2 + h) * hhalf) + lane;
+        frag_t hbuf[2][2][P];
+        auto load_ks = [&](int ks, frag_t (&dst)[2][P]) {
           const int ksa = w * KS + ks;
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) dst[nt][p] = hp[((ksa * 2 + nt) * 3 + p) * 64];
+            for (int p = 0; p < P; ++p) dst[nt][p] = hp[((ksa * 2 + nt) * P + p) * 64];
         };
         load_ks(0, hbuf[0]);
 #pragma unroll
@@ -401,10 +419,17 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
-            const ls_bf16x8* hb = hbuf[ks & 1][nt];
+            const frag_t* hb = hbuf[ks & 1][nt];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
               floatx4 s = acc[mt][nt];
+              if constexpr (P == 2) {
+                s = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[mt][ks][1], hb[0], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[mt][ks][0], hb[1], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[mt][ks][0], hb[0], s, 0, 0, 0);
+                acc[mt][nt] = s;
+                continue;
+              } else {
               s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][2], hb[0], s, 0, 0, 0);
               s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][1], hb[1], s, 0, 0, 0);
               s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[2], s, 0, 0, 0);
@@ -412,6 +437,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
               s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[1], s, 0, 0, 0);
               s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[mt][ks][0], hb[0], s, 0, 0, 0);
               acc[mt][nt] = s;
+              }
             }
           }
         }
@@ -441,7 +467,8 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
       }
       float gt[4];
 #pragma unroll
-      for (int gate = 0; gate < 4; ++gate) gt[gate] = t > 0 ? gxv[gate] + hsum[gate] : gxv[gate];
+      for (int gate = 0; gate < 4; ++gate)
+        gt[gate] = t > 0 ? gxv[gate] + (P == 2 ? hsum[gate] * gsc[gate] : hsum[gate]) : gxv[gate];
       const float ig = ls_sigmoid(gt[0]);
       const float fg = ls_sigmoid(gt[1]);
       const float gg = ls_tanh(gt[2]);
@@ -460,15 +487,26 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         const int ksa = g >> 2, qq = g & 3;
         const __amdgpu_buffer_rsrc_t hr =
             ls_rsrc(a.hseq + ((long long)t * 2 + h) * hhalf, (unsigned)(hhalf * 4));
-        const unsigned off = (unsigned)((ksa * 2 + nt) * 3 * 1024 + (qq * 16 + c16) * 16);
+        const unsigned off = (unsigned)((ksa * 2 + nt) * P * 1024 + (qq * 16 + c16) * 16);
         float hv[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) hv[i] = hs[lane][i];
-        ls_bf16x8 pl[3];
-        ls_split8(hv, pl);
+        ls_u32x4 pl[P];
+        if constexpr (P == 2) {
+          unsigned hh[4], mm[4];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u32x4, pl[p]), hr, off + p * 1024, 0, LS_SC1);
+          for (int i = 0; i < 4; ++i) split2_h(hv[2 * i] * 16384.0f, hv[2 * i + 1] * 16384.0f, hh[i], mm[i]);
+          pl[0] = (ls_u32x4){hh[0], hh[1], hh[2], hh[3]};
+          pl[1] = (ls_u32x4){mm[0], mm[1], mm[2], mm[3]};
+        } else {
+          ls_bf16x8 pb[3];
+          ls_split8(hv, pb);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) pl[p] = __builtin_bit_cast(ls_u32x4, pb[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+          __builtin_amdgcn_raw_buffer_store_b128(pl[p], hr, off + p * 1024, 0, LS_SC1);
       }
       if (w == 0 && t + 1 < a.T) {
         pend_h = h;
@@ -491,7 +529,10 @@ bool lstm_seq_ok(int H) {
   return ks == 2 || ks == 4 || ks == 8 || ks == 12;
 }
 
-long long lstm_seq_packed_bytes(int H) { return (long long)4 * H * H * 3 * 2; }
+// planes 3 (x6) or 2 (h3: + 1 / row scale per gate row, 4H floats)
+long long lstm_seq_packed_bytes(int H, int planes) {
+  return (long long)4 * H * H * planes * 2 + (planes == 2 ? (long long)4 * H * 4 : 0);
+}
 
 static inline unsigned short ls_f2bf(float f) {
   unsigned u;
@@ -506,15 +547,34 @@ static inline float ls_bf2f(unsigned short h) {
   return f;
 }
 
-// w: torch weight_hh [4H][H] (rows i, f, g, o).  out: [g][wave][mt][ks][plane][lane][8] bf16
-void lstm_seq_pack(const float* w, unsigned short* out, int H) {
+static inline unsigned short ls_f2h(float f) {
+  const _Float16 h = (_Float16)f;
+  unsigned short u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+static inline float ls_h2f(unsigned short u) {
+  _Float16 h;
+  memcpy(&h, &u, 2);
+  return (float)h;
+}
+
+// w: torch weight_hh [4H][H] (rows i, f, g, o).  out: [g][wave][mt][ks][plane][lane][8] bf16 (planes
+// = 3) or fp16 of w * S_row (planes = 2, then 1 / S_row for the 4H rows in torch order)
+void lstm_seq_pack(const float* w, unsigned short* out, int H, int planes) {
   const int KS = H / 128, G = H / LS_U;
+  std::vector<float> rsc(planes == 2 ? (size_t)4 * H : 0, 1.f);
+  for (size_t row = 0; row < rsc.size(); ++row) {
+    float m = 0.f;
+    for (int k = 0; k < H; ++k) m = std::max(m, std::fabs(w[(long long)row * H + k]));
+    if (m > 0.f && std::isfinite(m)) rsc[row] = std::ldexp(1.f, 14 - std::max(-112, std::min(140, std::ilogb(m))));
+  }
   long long o = 0;
   for (int g = 0; g < G; ++g)
     for (int wv = 0; wv < LS_WAVES; ++wv)
       for (int mt = 0; mt < 2; ++mt)
         for (int ks = 0; ks < KS; ++ks)
-          for (int p = 0; p < 3; ++p)
+          for (int p = 0; p < planes; ++p)
             for (int lane = 0; lane < 64; ++lane)
               for (int j = 0; j < 8; ++j, ++o) {
                 const int m = lane & 15;
@@ -522,12 +582,22 @@ void lstm_seq_pack(const float* w, unsigned short* out, int H) {
                 const int row = (m & 3) * H + unit;
                 const int k = (wv * KS + ks) * 32 + 8 * (lane >> 4) + j;
                 const float v = w[(long long)row * H + k];
+                if (planes == 2) {
+                  const float vs = v * rsc[row];
+                  const unsigned short g0 = ls_f2h(vs);
+                  out[o] = p == 0 ? g0 : ls_f2h(vs - ls_h2f(g0));
+                  continue;
+                }
                 const unsigned short h0 = ls_f2bf(v);
                 const float r1 = v - ls_bf2f(h0);
                 const unsigned short h1 = ls_f2bf(r1);
                 const unsigned short h2 = ls_f2bf(r1 - ls_bf2f(h1));
                 out[o] = p == 0 ? h0 : p == 1 ? h1 : h2;
               }
+  if (planes == 2) {
+    float* inv = reinterpret_cast<float*>(out + o);
+    for (size_t row = 0; row < rsc.size(); ++row) inv[row] = 1.f / rsc[row];
+  }
 }
 
 long long lstm_seq_workspace_bytes(int H, int T) {
@@ -577,7 +647,8 @@ static int device_cus() {
 }
 
 int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
-                    hipStream_t st) {
+                    int planes, hipStream_t st) {
+  if (planes != 2 && planes != 3) return BC_ERR_ARG;
   if (!lstm_seq_ok(H)) return BC_ERR_UNSUPPORTED;
   const int G = H / LS_U;
   if (G > 256 || G > device_cus()) return BC_ERR_UNSUPPORTED;  // every workgroup must be resident
@@ -610,8 +681,10 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
     if (hipMemsetAsync(a.flags, 0, LS_FLAG_BYTES, st) != hipSuccess) return BC_ERR_LAUNCH;
 #define BC_LS_CASE(KS)                                                                      \
   case KS:                                                                                  \
-    if (halves)                                                                             \
-      hipLaunchKernelGGL(lstm_seq2_x6_kernel<KS>, dim3(G), dim3(256), 0, st, a);            \
+    if (planes == 2)                                                                        \
+      hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 2>), dim3(G), dim3(256), 0, st, a);       \
+    else if (halves)                                                                        \
+      hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 3>), dim3(G), dim3(256), 0, st, a);       \
     else                                                                                    \
       hipLaunchKernelGGL(lstm_seq_x6_kernel<KS>, dim3(G), dim3(256), 0, st, a);             \
     break;

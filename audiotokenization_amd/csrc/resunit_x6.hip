@@ -16,6 +16,8 @@
 //            needs no weight copies and no barrier, and Hs may reuse the whole phase-1 LDS
 //            (Bs + As): a 96 x 128 tile fits in 80 KiB, i.e. two workgroups per CU.
 // Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
+// P = 3: x6 (3 bf16 planes, 6 products); P = 2: h3 (2 block-scaled fp16 planes, 3 products; the k=7
+// input is scaled per staged chunk as in conv1d_x6.hip, h per workgroup tile from its block maximum).
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
@@ -35,8 +37,11 @@ struct RUExtra {
 
 __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int P>
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
+  static_assert(P == 2 || P == 3, "x6 or h3 operands");
+  typedef typename FragType<P>::type frag_t;
+  __shared__ unsigned smax[2][8];  // P == 2: per-wave block maxima (k=7 input chunks by parity; h tile)
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;
   constexpr int CI = (BN + 6 * RU_MAX_DIL + 31) / 32;  // 32-column B passes: ncol <= BN + 6 * d
@@ -51,9 +56,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 
   const int ncol = a.win;
   const int bplane = a.bstage;
-  unsigned char* Bs = smem_ru;                 // phase 1: [3][ncol][80 B]
-  unsigned char* As = smem_ru + 3 * bplane;    // phase 1: [2][3][QA][1 KiB]
-  unsigned char* Hs = smem_ru;                 // phase 2: [3][nck1][BN][64 B] (aliases Bs and As)
+  unsigned char* Bs = smem_ru;                 // phase 1: [P][ncol][80 B]
+  unsigned char* As = smem_ru + P * bplane;    // phase 1: [2][P][QA][1 KiB]
+  unsigned char* Hs = smem_ru;                 // phase 2: [P][nck1][BN][64 B] (aliases Bs and As)
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int nt_idx = wg % a.ntn;
@@ -76,7 +81,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 
   const int K = a.K;
   const int nsteps = a.nchunks * K;
-  const int a_pieces = 3 * QA;
+  const int a_pieces = P * QA;
 
   auto issue_a = [&](const float* w, int step, int buf) {
     const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)step * (a_pieces * 1024);
@@ -102,11 +107,37 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       bv1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
     }
   };
+  auto bmax_publish = [&](int par) {
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < CI; ++i) {
+      const unsigned u0 = __float_as_uint(fabsf(bv0[i])), u1 = __float_as_uint(fabsf(bv1[i]));
+      m = m > u0 ? m : u0;
+      m = m > u1 ? m : u1;
+    }
+    m = wave_max_u32(m);
+    if (lane == 0) smax[par][wave] = m;
+  };
+  auto bmax_scale = [&](int par) {
+    unsigned m = smax[par][0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = m > smax[par][w] ? m : smax[par][w];
+    return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
+  };
+  float xs = 1.f;  // P == 2: scale of the staged k=7 input chunk and of the phase-1 accumulator
   auto store_b = [&]() {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
       if (col < ncol) {
+        if constexpr (P == 2) {
+          unsigned h, m;
+          split2_h(bv0[i] * xs, bv1[i] * xs, h, m);
+          unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+          *reinterpret_cast<unsigned*>(p) = h;
+          *reinterpret_cast<unsigned*>(p + bplane) = m;
+          continue;
+        }
         unsigned h, m, l;
         split2(bv0[i], bv1[i], h, m, l);
         unsigned char* p = Bs + col * X6_PITCH + bp * 4;
@@ -127,8 +158,26 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   const int col_lane = wn * NT * 16 + (lane & 15);
   const int kgrp16 = (lane >> 4) * 16;
 
+  // P == 2: next chunk's scale = min(current, its block scale); the accumulator follows exactly
+  auto h3_next_scale = [&](int par) {
+    const float sn = bmax_scale(par);
+    if (sn < xs) {
+      const float rr = sn / xs;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] *= rr;
+      xs = sn;
+    }
+  };
+
   issue_a(a.w, 0, 0);
   load_b(0);
+  if constexpr (P == 2) {
+    bmax_publish(0);
+    lds_barrier();
+    xs = bmax_scale(0);
+  }
   store_b();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -141,16 +190,28 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
       const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
       const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
-      bf16x8_t bf[NT][3];
+      frag_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bf[j][p] = *reinterpret_cast<const bf16x8_t*>(Bcol + j * 16 * X6_PITCH + p * bplane);
+        for (int p = 0; p < P; ++p)
+          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * X6_PITCH + p * bplane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
-        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(Aq);
+        const frag_t a0 = *reinterpret_cast<const frag_t*>(Aq);
+        if constexpr (P == 2) {
+          const frag_t a1 = *reinterpret_cast<const frag_t*>(Aq + QA * 1024);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            floatx4 t = acc[i][j];
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bf[j][0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bf[j][1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bf[j][0], t, 0, 0, 0);
+            acc[i][j] = t;
+          }
+          continue;
+        } else {
         const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
         const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
 #pragma unroll
@@ -164,9 +225,12 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
           t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], t, 0, 0, 0);
           acc[i][j] = t;
         }
+        }
       }
       if (tap == K - 1 && c + 1 < a.nchunks) {
+        if constexpr (P == 2) bmax_publish((c + 1) & 1);
         lds_barrier();
+        if constexpr (P == 2) h3_next_scale((c + 1) & 1);
         store_b();
       }
       if (tap == 0 && K > 1 && c + 1 < a.nchunks)
@@ -182,30 +246,72 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   // registers here so they land while the bridge runs
   const bool p2 = wave < QA * NPW;
   const int mq = wave % QA, jg = wave / QA;
-  bf16x8_t w1f[KC1][3];
+  frag_t w1f[KC1][P];
 #pragma unroll
   for (int kc = 0; kc < KC1; ++kc)
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < P; ++p)
       w1f[kc][p] = (p2 && kc < r.nck1)
-                       ? *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const unsigned char*>(r.w1) +
-                                                            ((kc * 3 + p) * QA + mq) * 1024 + lane * 16)
-                       : bf16x8_t{};
+                       ? *reinterpret_cast<const frag_t*>(reinterpret_cast<const unsigned char*>(r.w1) +
+                                                          ((kc * P + p) * QA + mq) * 1024 + lane * 16)
+                       : frag_t{};
   // (Hs overwrites Bs and As: every wave has passed the last step's barrier, no copy is in flight)
   const int C = a.Cout;
   if (C < r.nck1 * X6_BKC) {  // zero the pad channels of the last chunk (never written below)
     const int g0 = (C % X6_BKC) / 8;
-    for (int idx = tid; idx < 3 * BN * 4; idx += 512) {
+    for (int idx = tid; idx < P * BN * 4; idx += 512) {
       const int p = idx / (BN * 4), n = (idx / 4) % BN, g = idx % 4;
       if (g >= g0)
         *reinterpret_cast<floatx4*>(Hs + p * r.hplane + (r.nck1 - 1) * (BN * 64) + hs_off(n, g)) =
             floatx4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  float hs = 1.f;  // P == 2: scale of the h tile (block maximum over all its channels and columns)
+  if constexpr (P == 2) {
+    // h = snake2(acc * (1 / (x scale * w7 row scale)) + b7), its block maximum, then the split below
+    const float xinv = 1.f / xs;
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int co = wm * MT * 16 + i * 16 + (lane >> 4) * 4;
+      if (co >= C) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float bias = a.bias ? a.bias[co + q] : 0.f;
+        const float sc = a.wsc[co + q] * xinv, sa = r.s2a[co + q], sb = r.s2b[co + q];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const float v = snake(acc[i][j][q] * sc + bias, sa, sb);
+          acc[i][j][q] = v;
+          const unsigned u = __float_as_uint(fabsf(v));
+          m = m > u ? m : u;
+        }
+      }
+    }
+    m = wave_max_u32(m);
+    if (lane == 0) smax[0][wave] = m;  // slot 0: its last phase-1 reader passed the final barrier
+    lds_barrier();
+    hs = bmax_scale(0);
+  }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int co = wm * MT * 16 + i * 16 + (lane >> 4) * 4;  // 4 consecutive channels co..co+3
     if (co >= C) continue;
+    if constexpr (P == 2) {
+      unsigned char* hrow = Hs + (co / X6_BKC) * (BN * 64) + (co % 8) * 2;
+      const int g = (co % X6_BKC) / 8;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * NT * 16 + j * 16 + (lane & 15);
+        unsigned h0, m0, h1, m1;
+        split2_h(acc[i][j][0] * hs, acc[i][j][1] * hs, h0, m0);
+        split2_h(acc[i][j][2] * hs, acc[i][j][3] * hs, h1, m1);
+        unsigned char* dst = hrow + hs_off(n, g);
+        *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){h0, h1};
+        *reinterpret_cast<u32x2_t*>(dst + r.hplane) = (u32x2_t){m0, m1};
+      }
+      continue;
+    }
     float bias[4], sa[4], sb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -249,10 +355,17 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       for (int kc = 0; kc < KC1; ++kc) {
         if (kc >= r.nck1) break;
         const unsigned char* src = Hs + kc * (BN * 64) + hs_off(n, lane >> 4);
-        bf16x8_t bf[3];
+        frag_t bf[P];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bf[p] = *reinterpret_cast<const bf16x8_t*>(src + p * r.hplane);
+        for (int p = 0; p < P; ++p) bf[p] = *reinterpret_cast<const frag_t*>(src + p * r.hplane);
         floatx4 t = acc2[0][j];
+        if constexpr (P == 2) {
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0], w1f[kc][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[1], w1f[kc][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0], w1f[kc][0], t, 0, 0, 0);
+          acc2[0][j] = t;
+          continue;
+        } else {
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][2], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1], w1f[kc][1], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[2], w1f[kc][0], t, 0, 0, 0);
@@ -260,9 +373,13 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1], w1f[kc][0], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][0], t, 0, 0, 0);
         acc2[0][j] = t;
+        }
       }
     }
-    conv_epilogue<1, NTW>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane);
+    if constexpr (P == 2)
+      conv_epilogue<1, NTW, true>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs);
+    else
+      conv_epilogue<1, NTW>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane);
   }
 }
 
@@ -286,36 +403,38 @@ static int ru_forced_cfg() {
   return v;
 }
 
-static size_t ru_lds(const X6Tile& t, int C, int d, int* bplane, int* hplane) {
+static size_t ru_lds(const X6Tile& t, int C, int d, int P, int* bplane, int* hplane) {
   const int ncol = x6_ncol(t, 7, 1, d);
   *bplane = (ncol * X6_PITCH + 15) / 16 * 16;
   *hplane = (C + X6_BKC - 1) / X6_BKC * x6_BN(t) * 64;
-  const size_t ph1 = 3 * (size_t)*bplane + 2 * 3 * (size_t)t.WM * t.MT * 1024;  // Bs + As
-  const size_t ph2 = 3 * (size_t)*hplane;                                         // Hs
+  const size_t ph1 = P * (size_t)*bplane + 2 * P * (size_t)t.WM * t.MT * 1024;  // Bs + As
+  const size_t ph2 = P * (size_t)*hplane;                                         // Hs
   return ph1 > ph2 ? ph1 : ph2;
 }
 
+// mode 1 (x6) -> cfg 1xx, mode 3 (h3) -> cfg 3xx (same tile table)
 int resunit_select_cfg(int C, int d, int mode) {
-  if (mode != 1 || C < 16 || C % 16 || d <= 0) return -1;
+  if ((mode != 1 && mode != 3) || C < 16 || C % 16 || d <= 0) return -1;
+  const int P = mode == 3 ? 2 : 3;
   const int forced = ru_forced_cfg();
   for (int cfg : kRUCandidates) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
     if (d > RU_MAX_DIL) return -1;
     int bp, hp;
-    const size_t lds = ru_lds(t, C, d, &bp, &hp);
+    const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
     if (forced ? (cfg != forced || lds > 160 * 1024) : lds > RU_LDS_MAX) continue;
-    return cfg;
+    return cfg + (P == 2 ? 200 : 0);
   }
   return -1;
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int P>
 static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st) {
   constexpr int BN = 16 * NT * WN;
   const X6Tile t{MT, NT, WM, WN};
   int bplane, hplane;
-  const size_t lds = ru_lds(t, a.Cout, a.d, &bplane, &hplane);
+  const size_t lds = ru_lds(t, a.Cout, a.d, P, &bplane, &hplane);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   a.win = x6_ncol(t, 7, 1, a.d);
   a.bstage = bplane;
@@ -329,7 +448,14 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
   if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
-  hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  if (P == 2) {  // 1 / row scales after each packed weight's planes (conv1d_x6.hip x6_pack_weight)
+    constexpr int QA = MT * WM;
+    a.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
+                                           (long long)a.nchunks * 7 * P * QA * 1024);
+    e.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(r.w1) +
+                                           (long long)r.nck1 * P * QA * 1024);
+  }
+  hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
@@ -348,18 +474,22 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
   e.Cout = C; e.Nout = T; e.yT = T; e.ostride = 1; e.ooff = 0; e.epi = 0;
   e.vec = conv_epilogue_vec_ok(e);
   RUExtra r{w1, s2a, s2b, 0, 0};
+#define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
+  case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \
+  case 300 + ID: return launch_ru<MT, NT, WM, WN, 2>(a, e, r, B, st);
   switch (cfg) {
-    case 111: return launch_ru<3, 1, 1, 8>(a, e, r, B, st);
-    case 110: return launch_ru<4, 1, 1, 8>(a, e, r, B, st);
-    case 116: return launch_ru<3, 1, 2, 4>(a, e, r, B, st);
-    case 112: return launch_ru<2, 1, 1, 8>(a, e, r, B, st);
-    case 113: return launch_ru<1, 1, 1, 8>(a, e, r, B, st);
-    case 109: return launch_ru<6, 1, 1, 8>(a, e, r, B, st);
-    case 106: return launch_ru<3, 2, 1, 8>(a, e, r, B, st);
-    case 104: return launch_ru<6, 2, 1, 8>(a, e, r, B, st);
-    case 105: return launch_ru<4, 2, 1, 8>(a, e, r, B, st);
-    case 117: return launch_ru<4, 1, 2, 4>(a, e, r, B, st);
+    BC_RU_CASES(11, 3, 1, 1, 8)
+    BC_RU_CASES(10, 4, 1, 1, 8)
+    BC_RU_CASES(16, 3, 1, 2, 4)
+    BC_RU_CASES(12, 2, 1, 1, 8)
+    BC_RU_CASES(13, 1, 1, 1, 8)
+    BC_RU_CASES(9, 6, 1, 1, 8)
+    BC_RU_CASES(6, 3, 2, 1, 8)
+    BC_RU_CASES(4, 6, 2, 1, 8)
+    BC_RU_CASES(5, 4, 2, 1, 8)
+    BC_RU_CASES(17, 4, 1, 2, 4)
   }
+#undef BC_RU_CASES
   return BC_ERR_ARG;
 }
 

@@ -52,13 +52,14 @@ CONFIGS = {
 def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
-    if kname.startswith("conv1d_x6_kernel") and len(targs) >= 5 and targs[4] == "1":  # P = 1 plane
+    planes = targs[4] if kname.startswith(("conv1d_x6_kernel", "resunit_x6_kernel")) and len(targs) >= 5 else None
+    if planes == "1":
         return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"
-    if kname.startswith("conv1d_x6_kernel") and len(targs) >= 5 and targs[4] == "2":  # h3: 2 fp16 planes
+    if planes == "2":
         return (BF16_MFMA_PEAK_TFLOPS / H3_PRODUCTS, H3_PRODUCTS,
                 "2xfp16 split (h3): every fp32 multiply-add costs 3 fp16 MFMA multiply-adds (dense FP16 MFMA peak "
                 "= BF16's), so the fp32-equivalent ceiling is the dense FP16 MFMA peak / 3")
-    if kname.startswith("conv1d_x6_kernel"):
+    if planes == "3":
         return (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS, X6_PRODUCTS,
                 "3xbf16 split: every fp32 multiply-add costs 6 bf16 MFMA multiply-adds, so the fp32-equivalent "
                 "ceiling is the dense BF16 MFMA peak / 6")
@@ -79,7 +80,7 @@ def parse():
     p.add_argument("--no-kernel-timer", action="store_true")
     p.add_argument("--cpu-clips", type=int, default=1)
     p.add_argument("--precision", choices=["fp32", "x6", "bf16", "h3"], default=None,
-                   help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or x6)")
+                   help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or h3)")
     a = p.parse_args()
     c = CONFIGS[a.config]
     a.batch = a.batch or c["batch"]

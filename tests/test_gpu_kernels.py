@@ -248,11 +248,12 @@ def test_h3_block_scaling(dev, Cin, K, pw):
 @pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, False, 1, 700), (96, 3, False, 2, 513),
                                            (64, 9, False, 2, 300), (16, 3, True, 2, 257), (64, 1, False, 1, 260),
                                            (96, 9, True, 1, 999), (32, 1, False, 3, 64)])
-def test_resunit_fused(dev, C, d, causal, B, T):
-    """bc_resunit_fwd (one launch per ResidualUnit, x6) against the oracle: plain output, and the dual
-    raw + next-Snake output the encoder flow uses."""
+@pytest.mark.parametrize("ru_prec", ["x6", "h3"])
+def test_resunit_fused(dev, C, d, causal, B, T, ru_prec):
+    """bc_resunit_fwd (one launch per ResidualUnit, x6 or h3) against the oracle: plain output, and the
+    dual raw + next-Snake output the encoder flow uses."""
     old = L.precision_mode()
-    L.set_precision("x6")
+    L.set_precision(ru_prec)
     try:
         g = torch.Generator().manual_seed(C * 10 + d)
         ru = BL.ResidualUnit(C, dilation=d, causal=causal)
