@@ -173,7 +173,8 @@ CONV_CFGS = {t * 4 + b: _TILES[t] + (_BKC[b],) for t in range(5) for b in range(
 X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 4, 2), (2, 2, 4, 2), (6, 2, 1, 8),
                                               (4, 2, 1, 8), (3, 2, 1, 8), (2, 2, 1, 8), (1, 2, 1, 8), (6, 1, 1, 8),
                                               (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8),
-                                              (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4)])}
+                                              (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4),
+                                              (8, 2, 2, 4), (4, 4, 4, 2)])}
 
 
 def conv_kernel_name(cfg: int, taps: int = 0) -> str:

@@ -20,9 +20,9 @@ BUILD = os.path.join(PKG_DIR, "_build")
 LIB = os.path.join(PKG_DIR, "libbigcodec_hip.so")
 ARCH = os.environ.get("BIGCODEC_ARCH", "gfx950")
 
-SOURCES = ["conv1d.hip", "conv1d_x6.hip", "resunit_x6.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip",
+SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip", "conv1d_x6_p3.hip", "resunit_x6.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip",
            "vq.hip", "probe.hip", "abi.hip"]
-HEADERS = ["bc_common.h", "bc_internal.h", "conv_epilogue.h", "x6_common.h"]
+HEADERS = ["bc_common.h", "bc_internal.h", "conv_epilogue.h", "x6_common.h", "conv1d_x6_kernel.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
 
@@ -66,7 +66,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise RuntimeError(f"hipcc failed for {src}:\n{res.stderr}")
         return obj
 
-    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8, 16)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]

@@ -1,3 +1,6 @@
+// Host logic of the x6 / h3 / bf16 conv kernels (tile selection, weight packing, launch); the kernel
+// template is in conv1d_x6_kernel.h.
+//
 // Conv1d with fp32-accurate "3 x bf16" MFMA (x6 mode) for gfx950.
 //
 // Same GEMM and epilogue as conv1d.hip (reference: vq/module.py:11-72 and its callers), but the
@@ -25,322 +28,9 @@
 
 #include "bc_common.h"
 #include "bc_internal.h"
-#include "conv_epilogue.h"
-#include "x6_common.h"
+#include "conv1d_x6_kernel.h"
 
 namespace bc {
-
-// P = operand planes: 3 (x6, fp32-accurate), 2 ("h3": two fp16 planes, three products, fp32-class
-// accuracy at half the x6 MFMA count, x6_common.h) or 1 (plain bf16 products: the "bf16" precision
-// mode of BASELINE config 5, activations still stored fp32).
-// h3 scaling: each staged 32-channel B chunk gets a power-of-two scale from its block maximum (a wave
-// reduction + an LDS exchange folded into the barrier in front of the chunk's store); the scale only
-// ever decreases within a workgroup, the accumulator is rescaled (exactly) when it does, and the
-// epilogue multiplies by 1 / (x scale * per-row weight scale).
-// PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
-template <int MT, int NT, int WM, int WN, int P, bool PW>
-// NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
-// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
-__global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
-  constexpr int BM = 16 * MT * WM;
-  constexpr int BN = 16 * NT * WN;
-  constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
-  constexpr int CI = PW ? BN / 32 : X6_MAXCOL_ITERS;  // 32-column B passes per chunk
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
-  __shared__ unsigned smax[2][8];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
-  typedef typename FragType<P>::type frag_t;
-
-  const int ncol = a.win;                // columns of the input tile
-  const int bplane = a.bstage;           // bytes per B plane (multiple of 16)
-  unsigned char* Bs = smem_x6;                            // [3][ncol][80 B]
-  unsigned char* As = smem_x6 + P * bplane;               // [2][P][QA][1 KiB]
-
-  const int wg = xcd_remap(blockIdx.x, a.nwg);
-  const int mt_idx = wg % a.ntm;
-  const int rest = wg / a.ntm;
-  const int nt_idx = rest % a.ntn;
-  const int b = rest / a.ntn;
-  const int m0 = mt_idx * BM;
-  const int n0 = nt_idx * BN;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave % WM;
-  const int wn = wave / WM;
-
-  const unsigned long long xb_u = (unsigned long long)(a.x + (long long)b * a.xbs);
-  const unsigned xb_lo = __builtin_amdgcn_readfirstlane((unsigned)xb_u);
-  const unsigned xb_hi = __builtin_amdgcn_readfirstlane((unsigned)(xb_u >> 32));
-  const int xbytes = __builtin_amdgcn_readfirstlane((a.ps ? a.cin0 : a.Cin) * a.Tin * 4);
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((unsigned long long)xb_hi << 32) | xb_lo), 0, xbytes, 0x00020000);
-  const int in0 = n0 * a.s - a.pl;
-  const int tstep = a.ps ? a.ps : 1;  // input samples per B-tile column
-
-  const int K = a.K;
-  const int nsteps = a.nchunks * K;
-  const int a_pieces = P * QA;
-  const unsigned char* wblk = reinterpret_cast<const unsigned char*>(a.w) +
-                              (long long)mt_idx * a.nchunks * K * (a_pieces * 1024);
-
-  auto issue_a = [&](int step, int buf) {
-    const unsigned char* src = wblk + (long long)step * (a_pieces * 1024);
-    unsigned char* dst = As + buf * (a_pieces * 1024);
-    for (int q = wave; q < a_pieces; q += 8)
-      __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
-                                       16, 0, 0);
-  };
-
-  // B staging: thread -> (channel pair p, column lane cl); columns cl + 32*i, i < CI
-  const int bp = tid >> 5;       // 0..15
-  const int bcl = tid & 31;
-  float bv0[CI], bv1[CI];
-  auto load_b = [&](int chunk, float (&v0)[CI], float (&v1)[CI]) {
-    const int ci0 = chunk * X6_BKC + 2 * bp;
-    // channel (row) -> input channel and the input time of column 0; phase mode: row ci' is phase
-    // r = ci' % ps of channel ci' / ps, column m reads sample (n0 + m) * ps + r - pl
-    int ch0 = ci0, ch1 = ci0 + 1, tb0 = in0, tb1 = in0;
-    if (a.ps) {
-      ch0 = ci0 / a.ps;
-      ch1 = (ci0 + 1) / a.ps;
-      tb0 = n0 * a.ps + (ci0 - ch0 * a.ps) - a.pl;
-      tb1 = n0 * a.ps + (ci0 + 1 - ch1 * a.ps) - a.pl;
-    }
-#pragma unroll
-    for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
-      const int t0 = tb0 + col * tstep, t1 = tb1 + col * tstep;
-      const bool cin = col < ncol;
-      const unsigned o0 = (cin && ci0 < a.Cin && t0 >= 0 && t0 < a.Tin) ? (unsigned)((ch0 * a.Tin + t0) * 4) : 0xfffffff0u;
-      const unsigned o1 =
-          (cin && ci0 + 1 < a.Cin && t1 >= 0 && t1 < a.Tin) ? (unsigned)((ch1 * a.Tin + t1) * 4) : 0xfffffff0u;
-      v0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
-      v1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
-    }
-  };
-  // P == 2: publish this wave's block maximum of a chunk's staged values / read the block's scale
-  auto bmax_publish = [&](const float (&w0)[CI], const float (&w1)[CI], int par) {
-    unsigned m = 0;
-#pragma unroll
-    for (int i = 0; i < CI; ++i) {
-      const unsigned u0 = __float_as_uint(fabsf(w0[i])), u1 = __float_as_uint(fabsf(w1[i]));
-      m = m > u0 ? m : u0;
-      m = m > u1 ? m : u1;
-    }
-    m = wave_max_u32(m);
-    if (lane == 0) smax[par][wave] = m;
-  };
-  auto bmax_scale = [&](int par) {
-    unsigned m = smax[par][0];
-#pragma unroll
-    for (int w = 1; w < 8; ++w) m = m > smax[par][w] ? m : smax[par][w];
-    return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
-  };
-  float xs = 1.f;  // P == 2: scale of the staged chunk and of the accumulator
-  auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI]) {
-#pragma unroll
-    for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
-      if (col < ncol) {
-        const float v0 = w0[i], v1 = w1[i];
-        if constexpr (P == 2) {
-          unsigned h, m;
-          split2_h(v0 * xs, v1 * xs, h, m);
-          unsigned char* p = Bs + col * X6_PITCH + bp * 4;
-          *reinterpret_cast<unsigned*>(p) = h;
-          *reinterpret_cast<unsigned*>(p + bplane) = m;
-          continue;
-        }
-        const unsigned h = pk_bf16(v0, v1);
-        unsigned char* p = Bs + col * X6_PITCH + bp * 4;
-        *reinterpret_cast<unsigned*>(p) = h;
-        if (P == 3) {
-          const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
-          const unsigned m = pk_bf16(r0, r1);
-          const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
-          const unsigned l = pk_bf16(s0, s1);
-          *reinterpret_cast<unsigned*>(p + bplane) = m;
-          *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
-        }
-      }
-    }
-  };
-
-  floatx4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // P == 2, at a chunk boundary (the previous chunk's B tile is no longer read): the next chunk's
-  // scale = min(current, its block scale); the accumulator follows exactly (powers of two)
-  auto h3_next_scale = [&](int par) {
-    const float sn = bmax_scale(par);
-    if (sn < xs) {
-      const float r = sn / xs;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] *= r;
-      xs = sn;
-    }
-  };
-
-  const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
-  const int kgrp16 = (lane >> 4) * 16;
-
-  // one K32 step: this wave's MT x NT tiles += A(step) * B(tap-shifted columns)
-  auto compute = [&](int step, int tap) {
-      const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
-      const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
-      frag_t bf[NT][P];
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
-        const frag_t a0 = *reinterpret_cast<const frag_t*>(Aq);
-        if constexpr (P == 2) {
-          const frag_t a1 = *reinterpret_cast<const frag_t*>(Aq + QA * 1024);
-#pragma unroll
-          for (int j = 0; j < NT; ++j) {
-            floatx4 t = acc[i][j];
-            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][1], a0, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a1, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a0, t, 0, 0, 0);
-            acc[i][j] = t;
-          }
-          continue;
-        } else {
-        if (P == 1) {
-#pragma unroll
-          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
-          continue;
-        }
-        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
-        const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          // operands swapped (input as A): the tile comes out transposed, see conv_epilogue.h
-          floatx4 t = acc[i][j];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
-          acc[i][j] = t;
-        }
-        }
-      }
-  };
-
-  // prologue: A(step 0), B(chunk 0)
-  issue_a(0, 0);
-  load_b(0, bv0, bv1);
-  if constexpr (P == 2) {
-    bmax_publish(bv0, bv1, 0);
-    lds_barrier();
-    xs = bmax_scale(0);
-  }
-  store_b(bv0, bv1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  if constexpr (PW) {
-    // Pointwise conv (K = 1): one step per chunk, so the B loads run two chunks ahead in two
-    // register sets (chunk c + 2 is issued while chunk c computes and chunk c + 1 is stored).
-    float bw0[CI], bw1[CI];
-    if (a.nchunks > 1) load_b(1, bw0, bw1);
-    auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
-      if (c + 1 < a.nchunks && !(a.dbg & 1)) issue_a(c + 1, (c + 1) & 1);
-      if (c + 2 < a.nchunks && !(a.dbg & 2)) load_b(c + 2, p0v, p1v);
-      compute(c, 0);
-      if (c + 1 < a.nchunks) {
-        if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
-        lds_barrier();  // every wave is done reading this chunk's B tile
-        if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-        if (!(a.dbg & 4)) store_b(n0v, n1v);
-      }
-      // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
-      if (c + 2 < a.nchunks)
-        wait_vmcnt<2 * CI>();
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-    };
-    for (int c = 0; c < a.nchunks; c += 2) {
-      step1(c, bw0, bw1, bv0, bv1);
-      if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
-    }
-  } else {
-    for (int c = 0; c < a.nchunks; ++c) {
-      for (int tap = 0; tap < K; ++tap) {
-        const int step = c * K + tap;
-        if (step + 1 < nsteps && !(a.dbg & 1)) issue_a(step + 1, (step + 1) & 1);
-        if (tap == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
-        compute(step, tap);
-        if (tap == K - 1 && c + 1 < a.nchunks) {
-          if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
-          lds_barrier();  // every wave is done reading this chunk's B tile
-          if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-          if (!(a.dbg & 4)) store_b(bv0, bv1);
-        }
-        // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
-        // tap 0 of a multi-tap chunk the 2*CI B loads of the next chunk were issued after it and
-        // may stay in flight (vmcnt retires in issue order); they are consumed at the chunk's last
-        // tap, where the compiler waits for their registers itself.
-        if (tap == 0 && K > 1 && c + 1 < a.nchunks)
-          wait_vmcnt<2 * CI>();
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-      }
-    }
-  }
-
-  if (!(a.dbg & 8)) {
-    if constexpr (P == 2)
-      conv_epilogue<MT, NT, true>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
-    else
-      conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// host side
-// ------------------------------------------------------------------------------------------------
-// cfg ids 100..: index into this table
-static const X6Tile kX6Tiles[] = {
-    {4, 4, 2, 4},  // 100: BM=128 BN=256  (Cout >= 128, stride 1)
-    {4, 2, 2, 4},  // 101: BM=128 BN=128  (Cout >= 128, stride 2)
-    {4, 2, 4, 2},  // 102: BM=256 BN=64   (Cout >= 256, stride >= 3)
-    {2, 2, 4, 2},  // 103: BM=128 BN=64   (Cout >= 128, stride >= 3)
-    {6, 2, 1, 8},  // 104: BM=96  BN=256
-    {4, 2, 1, 8},  // 105: BM=64  BN=256
-    {3, 2, 1, 8},  // 106: BM=48  BN=256
-    {2, 2, 1, 8},  // 107: BM=32  BN=256
-    {1, 2, 1, 8},  // 108: BM=16  BN=256
-    {6, 1, 1, 8},  // 109: BM=96  BN=128
-    {4, 1, 1, 8},  // 110: BM=64  BN=128
-    {3, 1, 1, 8},  // 111: BM=48  BN=128
-    {2, 1, 1, 8},  // 112: BM=32  BN=128
-    {1, 1, 1, 8},  // 113: BM=16  BN=128
-    {6, 2, 2, 4},  // 114: BM=192 BN=128  (Cout = 192k, stride <= 2)
-    {6, 1, 2, 4},  // 115: BM=192 BN=64
-    {3, 1, 2, 4},  // 116: BM=96  BN=64   (one-launch ResidualUnit at C = 96, two workgroups per CU)
-    {4, 1, 2, 4},  // 117: BM=128 BN=64   (two workgroups per CU)
-};
-constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
-
-static inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
-  const size_t bplane = (size_t)((ncol * X6_PITCH + 15) / 16 * 16);
-  return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
-}
 
 // cfg ids: 100 + tile (x6, three planes), 200 + tile (bf16, one plane), 300 + tile (h3, two fp16
 // planes); + 1000 * s for a stride-s
@@ -418,8 +108,27 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   return -1;
 }
 
+// Measured tile preferences of the h3 (two-plane) kernel (tools/tile_sweep.sh, profiles/
+// r01f_h3_tile_sweep.txt), where they differ from the x6 ones:
+//   pointwise, Cout % 192 == 0     -> 114 (192 x 128): C = 192 / 384 / 768 and the LSTM input
+//                                     projection, 10-20 % under 101 / 116
+//   stride 2, Cout % 192 == 0 and <= 384 -> 115 (192 x 64, direct strided B tile): -15 %
+//   stride >= 3, Cout % 256 == 0   -> 102 (256 x 64, direct strided B tile, not phase-decomposed):
+//                                     the stride-5 downsampling convs, -20 %
+static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
+  (void)Cin;
+  if (s == 1 && K == 1 && Cout % 192 == 0) return 114;
+  if (s == 2 && d == 1 && Cout % 192 == 0 && Cout <= 384) return 115;
+  if (s >= 3 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[2], K, s, d) <= 32 * X6_MAXCOL_ITERS) return 102;
+  return -1;
+}
+
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
+  if (planes == 2 && x6_occ_pref() == 0) {
+    const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
+    if (c >= 0) return c + 200;
+  }
   if (planes >= 2 && x6_occ_pref() == 0) {
     const int c = x6_preferred_cfg(Cout, Cin, K, s, d);
     if (c >= 0) return c + (planes == 2 ? 200 : 0);
@@ -570,44 +279,6 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
   }
 }
 
-// BC_X6_PW=0 runs pointwise convs on the general kernel (A/B timing).
-static bool x6_pw_on() {
-  static const bool v = [] {
-    const char* e = getenv("BC_X6_PW");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
-
-template <int MT, int NT, int WM, int WN, int P>
-static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
-  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
-  const X6Tile t{MT, NT, WM, WN};
-  const int ncol = x6_ncol(t, a.K, a.s, a.d);
-  if (ncol > 32 * X6_MAXCOL_ITERS) return BC_ERR_UNSUPPORTED;
-  a.ntm = (a.Cout + BM - 1) / BM;
-  a.ntn = (a.Nout + BN - 1) / BN;
-  a.nchunks = (a.Cin + X6_BKC - 1) / X6_BKC;
-  a.win = ncol;
-  a.bstage = (ncol * X6_PITCH + 15) / 16 * 16;
-  const long long nwg = (long long)a.ntm * a.ntn * B;
-  if (nwg <= 0) return BC_OK;
-  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
-  if ((long long)(a.ps ? a.cin0 : a.Cin) * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
-  a.nwg = (int)nwg;
-  a.wsc = P == 2 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
-                                                  (long long)a.ntm * a.nchunks * a.K * P * t.WM * t.MT * 1024)
-                 : nullptr;
-  const size_t lds = x6_lds(t, ncol, P);
-  if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  if (a.K == 1 && ncol == BN && x6_pw_on())
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
-  else
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), lds, st, a);
-  BC_CHECK_LAUNCH();
-  return BC_OK;
-}
-
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
   static const int dbg = [] {
     const char* e = getenv("BC_X6_DEBUG");
@@ -624,31 +295,12 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
     a.s = 1;
     cfg = cfg_base(cfg);
   }
-#define BC_X6_CASES(ID, MT, NT, WM, WN)                                \
-  case 100 + ID: return launch_x6<MT, NT, WM, WN, 3>(a, B, st);        \
-  case 200 + ID: return launch_x6<MT, NT, WM, WN, 1>(a, B, st);        \
-  case 300 + ID: return launch_x6<MT, NT, WM, WN, 2>(a, B, st);
-  switch (cfg) {
-    BC_X6_CASES(0, 4, 4, 2, 4)
-    BC_X6_CASES(1, 4, 2, 2, 4)
-    BC_X6_CASES(2, 4, 2, 4, 2)
-    BC_X6_CASES(3, 2, 2, 4, 2)
-    BC_X6_CASES(4, 6, 2, 1, 8)
-    BC_X6_CASES(5, 4, 2, 1, 8)
-    BC_X6_CASES(6, 3, 2, 1, 8)
-    BC_X6_CASES(7, 2, 2, 1, 8)
-    BC_X6_CASES(8, 1, 2, 1, 8)
-    BC_X6_CASES(9, 6, 1, 1, 8)
-    BC_X6_CASES(10, 4, 1, 1, 8)
-    BC_X6_CASES(11, 3, 1, 1, 8)
-    BC_X6_CASES(12, 2, 1, 1, 8)
-    BC_X6_CASES(13, 1, 1, 1, 8)
-    BC_X6_CASES(14, 6, 2, 2, 4)
-    BC_X6_CASES(15, 6, 1, 2, 4)
-    BC_X6_CASES(16, 3, 1, 2, 4)
-    BC_X6_CASES(17, 4, 1, 2, 4)
+  const int tile = cfg_base(cfg) % 100;
+  switch (cfg_planes(cfg)) {
+    case 1: return x6_launch_tile<1>(a, B, tile, st);
+    case 2: return x6_launch_tile<2>(a, B, tile, st);
+    case 3: return x6_launch_tile<3>(a, B, tile, st);
   }
-#undef BC_X6_CASES
   return BC_ERR_ARG;
 }
 

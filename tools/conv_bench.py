@@ -55,7 +55,9 @@ def main():
     lib = L.load()
     chosen = lib.bc_conv1d_select_cfg(a.cout, a.cin, a.k, a.s, a.d, L.precision_mode())
     if a.cfg == "all":  # every x6 tile (and, for stride >= 2, every phase-decomposed one)
-        cfgs = sorted(L.X6_CFGS) + ([1000 * a.s + c for c in sorted(L.X6_CFGS)] if a.s >= 2 else [])
+        base = {"x6": 0, "bf16": 100, "h3": 200}[a.precision]
+        tiles = [c + base for c in sorted(L.X6_CFGS)]
+        cfgs = tiles + ([1000 * a.s + c for c in tiles] if a.s >= 2 else [])
     else:
         cfgs = [int(c) for c in a.cfg.split(",") if c] or [chosen]
     st = torch.cuda.current_stream().cuda_stream

@@ -1,7 +1,7 @@
-# Tile sweep of the encoder conv shapes (every x6 cfg per shape): profiles/r01_tile_sweep.txt
+# Tile sweep of the encoder conv shapes (every tile of the chosen precision per shape): profiles/r01_tile_sweep.txt
 set -e
 mkdir -p gpurun_out
-run() { timeout -k 10 300 python tools/conv_bench.py --iters 5 --cfg all "$@" >> gpurun_out/sweep.log 2>&1; }
+run() { timeout -k 10 300 python tools/conv_bench.py --iters 5 --cfg all --precision ${PRECISION:-h3} "$@" >> gpurun_out/sweep.log 2>&1; }
 run --cin 48 --cout 96 --k 4 --s 2 --T 120000 --snake
 run --cin 96 --cout 192 --k 4 --s 2 --T 60000 --snake
 run --cin 192 --cout 384 --k 4 --s 2 --T 30000 --snake
