@@ -143,7 +143,7 @@ class Conv1dWN(_WNParams, nn.Module):
         if tm is not None:
             flops = 2.0 * B * self.out_channels * Cin * self.kernel_size * Tout
             nbytes = 4.0 * (x.numel() + y.numel() * (1 + (residual is not None) + dual))
-            tm.end(ev, L.conv_kernel_name(cfg, self.kernel_size), flops, nbytes)
+            tm.end(ev, L.conv_kernel_name(cfg, self.kernel_size, self.stride, self.dilation), flops, nbytes)
         return (y, y2) if dual else y
 
     def forward(self, x):

@@ -95,7 +95,7 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   auto fits2 = [](int tile, int K_, int s_, int d_) {  // two workgroups per CU: LDS <= 80 KiB
     const X6Tile& t = kX6Tiles[tile];
     const int ncol = x6_ncol(t, K_, s_, d_);
-    return ncol <= 32 * X6_MAXCOL_ITERS && x6_lds(t, ncol, 3) <= 80 * 1024;
+    return ncol <= 32 * X6_MAXCOL_ITERS && x6_lds(t, ncol, 3, s_) <= 80 * 1024;
   };
   if (s == 1 && K == 1) {
     if (Cout % 128 == 0) return 101;
@@ -108,17 +108,33 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   return -1;
 }
 
-// Measured tile preferences of the h3 (two-plane) kernel (tools/tile_sweep.sh, profiles/
-// r01f_h3_tile_sweep.txt), where they differ from the x6 ones:
-//   pointwise, Cout % 192 == 0     -> 114 (192 x 128): C = 192 / 384 / 768 and the LSTM input
-//                                     projection, 10-20 % under 101 / 116
+// Measured tile preferences of the h3 (two-plane) kernel (tools/tile_sweep.sh, tools/x6_tile_sweep2.sh /
+// 3.sh; profiles/r01f_h3_tile_sweep.txt, r01g_wide_tile_sweep*.txt), where they differ from the x6 ones:
+//   stride 1, K > 1, Cout % 192 == 0 -> 120 (192 x 256, 96 x 64 per wave, two taps per K-step):
+//                                     k7 C = 192 / 384 -9 / -14 % vs 109, decoder k7 1024 -> 1536 -8 %
+//   stride 1, K > 1, Cout == 768 or Cout % 256 == 0 (not % 192) -> 121 (256 x 256): k7 C = 768 -16 %,
+//                                     the final k3 1536 -> 1024 -16 %
+//   stride >= 3, d = 1, Cout % 256 == 0 -> phase-decomposed 121: the stride-5 downsampling convs -9..-14 %
+//                                     vs the direct strided 256 x 64 tile
+//   pointwise, Cout % 192 == 0     -> 114 (192 x 128): C = 192 / 384 / 768, 10-20 % under 101 / 116
+//                                     (the x256 tiles lose 20-30 % here), except Cout >= 2048 with
+//                                     Cout % 256 == 0 (the LSTM input projection) -> 121
 //   stride 2, Cout % 192 == 0 and <= 384 -> 115 (192 x 64, direct strided B tile): -15 %
-//   stride >= 3, Cout % 256 == 0   -> 102 (256 x 64, direct strided B tile, not phase-decomposed):
-//                                     the stride-5 downsampling convs, -20 %
 static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
-  if (s == 1 && K == 1 && Cout % 192 == 0) return 114;
+  if (s == 1 && K == 1) {
+    if (Cout >= 2048 && Cout % 256 == 0) return 121;
+    if (Cout % 192 == 0) return 114;
+  }
+  if (s == 1 && K > 1) {
+    const bool f320 = Cout % 192 == 0, f321 = Cout % 256 == 0;
+    auto fits = [&](int tile) { return x6_ncol(kX6Tiles[tile], K, 1, d) <= 32 * X6_MAXCOL_ITERS; };
+    if ((Cout == 768 || (f321 && !f320)) && fits(21)) return 121;
+    if (f320 && fits(20)) return 120;
+  }
   if (s == 2 && d == 1 && Cout % 192 == 0 && Cout <= 384) return 115;
+  if (s >= 3 && s <= 16 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[21], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS)
+    return 1000 * s + 121;
   if (s >= 3 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[2], K, s, d) <= 32 * X6_MAXCOL_ITERS) return 102;
   return -1;
 }
@@ -127,7 +143,7 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
   if (planes == 2 && x6_occ_pref() == 0) {
     const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
-    if (c >= 0) return c + 200;
+    if (c >= 0) return c + 200;  // (a phase-decomposed 1000 * s + tile keeps its phase factor)
   }
   if (planes >= 2 && x6_occ_pref() == 0) {
     const int c = x6_preferred_cfg(Cout, Cin, K, s, d);
@@ -178,7 +194,7 @@ static int x6_select_tile(int Cout, int Cin, int K, int s, int d, int planes) {
     const X6Tile& t = kX6Tiles[order[i]];
     const int ncol = x6_ncol(t, K, s, d);
     if (ncol > 32 * X6_MAXCOL_ITERS) continue;
-    if (x6_lds(t, ncol, planes) > (occ4[i] ? 80 : 160) * 1024) continue;
+    if (x6_lds(t, ncol, planes, s) > (occ4[i] ? 80 : 160) * 1024) continue;
     return planes_base(planes) + order[i];
   }
   return -1;

@@ -37,7 +37,9 @@ namespace bc {
 // ever decreases within a workgroup, the accumulator is rescaled (exactly) when it does, and the
 // epilogue multiplies by 1 / (x scale * per-row weight scale).
 // PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
-template <int MT, int NT, int WM, int WN, int P, bool PW>
+// TPS: taps per K-step of the multi-tap path (1 or 2): one A copy, one wait and one barrier cover
+// TPS (chunk, tap) units, i.e. BK = 32 * TPS per barrier.
+template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
 // one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
@@ -51,8 +53,12 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
 
   const int ncol = a.win;                // columns of the input tile
   const int bplane = a.bstage;           // bytes per B plane (multiple of 16)
-  unsigned char* Bs = smem_x6;                            // [3][ncol][80 B]
-  unsigned char* As = smem_x6 + P * bplane;               // [2][P][QA][1 KiB]
+  const int bpitch = a.bpitch;           // x6_common.h x6_pitch
+  const bool bswz = bpitch == 64;
+  // byte offset of 16-B channel group g (channels 8g..8g+7 of the chunk) of column col
+  auto bgrp = [&](int col, int g) { return col * bpitch + 16 * (bswz ? (g ^ ((col >> 1) & 3)) : g); };
+  unsigned char* Bs = smem_x6;                            // [P][ncol][bpitch]
+  unsigned char* As = smem_x6 + P * bplane;               // [2][TPS][P][QA][1 KiB]
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int mt_idx = wg % a.ntm;
@@ -78,15 +84,19 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   const int tstep = a.ps ? a.ps : 1;  // input samples per B-tile column
 
   const int K = a.K;
-  const int nsteps = a.nchunks * K;
+  const int kst = (K + TPS - 1) / TPS;  // K-steps per chunk
+  const int nsteps = a.nchunks * kst;
   const int a_pieces = P * QA;
   const unsigned char* wblk = reinterpret_cast<const unsigned char*>(a.w) +
                               (long long)mt_idx * a.nchunks * K * (a_pieces * 1024);
 
+  // A copy of K-step `step` = taps [TPS * tp, TPS * tp + TPS) of chunk c (consecutive packed blocks)
   auto issue_a = [&](int step, int buf) {
-    const unsigned char* src = wblk + (long long)step * (a_pieces * 1024);
-    unsigned char* dst = As + buf * (a_pieces * 1024);
-    for (int q = wave; q < a_pieces; q += 8)
+    const int c = step / kst, t0 = (step - c * kst) * TPS;
+    const int n = (K - t0 < TPS ? K - t0 : TPS) * a_pieces;
+    const unsigned char* src = wblk + (long long)(c * K + t0) * (a_pieces * 1024);
+    unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
+    for (int q = wave; q < n; q += 8)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);
   };
@@ -146,13 +156,13 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
         if constexpr (P == 2) {
           unsigned h, m;
           split2_h(v0 * xs, v1 * xs, h, m);
-          unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+          unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
           *reinterpret_cast<unsigned*>(p) = h;
           *reinterpret_cast<unsigned*>(p + bplane) = m;
           continue;
         }
         const unsigned h = pk_bf16(v0, v1);
-        unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+        unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
         *reinterpret_cast<unsigned*>(p) = h;
         if (P == 3) {
           const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
@@ -187,18 +197,18 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   };
 
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
-  const int kgrp16 = (lane >> 4) * 16;
 
-  // one K32 step: this wave's MT x NT tiles += A(step) * B(tap-shifted columns)
-  auto compute = [&](int step, int tap) {
-      const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
-      const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
+  // one K32 unit: this wave's MT x NT tiles += A(buffer buf, slot tt) * B(tap-shifted columns)
+  auto compute = [&](int buf, int tt, int tap) {
+      const unsigned char* Ab = As + buf * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
+      // (n-tile j adds 16 * s columns: the swizzle of a stride-1 tile repeats every 8 columns)
+      const unsigned char* Bcol = Bs + bgrp(col_lane + tap * a.d, lane >> 4);
       frag_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * a.s * X6_PITCH + p * bplane);
+          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * a.s * bpitch + p * bplane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
@@ -258,7 +268,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
       if (c + 1 < a.nchunks && !(a.dbg & 1)) issue_a(c + 1, (c + 1) & 1);
       if (c + 2 < a.nchunks && !(a.dbg & 2)) load_b(c + 2, p0v, p1v);
-      compute(c, 0);
+      compute(c & 1, 0, 0);
       if (c + 1 < a.nchunks) {
         if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
@@ -277,23 +287,30 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
     }
   } else {
+    const bool prio = a.dbg & 16;
     for (int c = 0; c < a.nchunks; ++c) {
-      for (int tap = 0; tap < K; ++tap) {
-        const int step = c * K + tap;
+      for (int tp = 0; tp < kst; ++tp) {
+        const int step = c * kst + tp;
         if (step + 1 < nsteps && !(a.dbg & 1)) issue_a(step + 1, (step + 1) & 1);
-        if (tap == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
-        compute(step, tap);
-        if (tap == K - 1 && c + 1 < a.nchunks) {
+        if (tp == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
+        if (prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int tt = 0; tt < TPS; ++tt) {
+          const int tap = tp * TPS + tt;
+          if (TPS == 1 || tap < K) compute(step & 1, tt, tap);
+        }
+        if (prio) __builtin_amdgcn_s_setprio(0);
+        if (tp == kst - 1 && c + 1 < a.nchunks) {
           if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
           if constexpr (P == 2) h3_next_scale((c + 1) & 1);
           if (!(a.dbg & 4)) store_b(bv0, bv1);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
-        // tap 0 of a multi-tap chunk the 2*CI B loads of the next chunk were issued after it and
+        // step 0 of a multi-step chunk the 2*CI B loads of the next chunk were issued after it and
         // may stay in flight (vmcnt retires in issue order); they are consumed at the chunk's last
-        // tap, where the compiler waits for their registers itself.
-        if (tap == 0 && K > 1 && c + 1 < a.nchunks)
+        // step, where the compiler waits for their registers itself.
+        if (tp == 0 && kst > 1 && c + 1 < a.nchunks)
           wait_vmcnt<2 * CI>();
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -335,12 +352,24 @@ inline constexpr X6Tile kX6Tiles[] = {
     {4, 1, 2, 4},  // 117: BM=128 BN=64   (two workgroups per CU)
     {8, 2, 2, 4},  // 118: BM=256 BN=128  (h3: fits where the x6 planes did not)
     {4, 4, 4, 2},  // 119: BM=256 BN=128
+    {6, 4, 2, 4},  // 120: BM=192 BN=256  (h3: 96 x 64 per wave)
+    {8, 4, 2, 4},  // 121: BM=256 BN=256
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
-inline size_t x6_lds(const X6Tile& t, int ncol, int planes) {
-  const size_t bplane = (size_t)((ncol * X6_PITCH + 15) / 16 * 16);
-  return planes * bplane + 2 * planes * (size_t)t.WM * t.MT * 1024;
+inline size_t x6_lds(const X6Tile& t, int ncol, int planes, int s, int tps = 1) {
+  const size_t bplane = (size_t)((ncol * x6_pitch(s) + 15) / 16 * 16);
+  return planes * bplane + 2 * tps * planes * (size_t)t.WM * t.MT * 1024;
+}
+
+// h3 kernels run the multi-tap path with two taps per K-step where the doubled A buffers fit the
+// tile's LDS budget (measured: -4 % on the k7 convs, profiles/r01g_tps_sweep.txt); BC_X6_TPS=1 disables it.
+inline int x6_tps() {
+  static const int v = [] {
+    const char* e = getenv("BC_X6_TPS");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return v;
 }
 
 // BC_X6_PW=0 runs pointwise convs on the general kernel (A/B timing).
@@ -362,7 +391,8 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   a.ntn = (a.Nout + BN - 1) / BN;
   a.nchunks = (a.Cin + X6_BKC - 1) / X6_BKC;
   a.win = ncol;
-  a.bstage = (ncol * X6_PITCH + 15) / 16 * 16;
+  a.bpitch = x6_pitch(a.s);
+  a.bstage = (ncol * a.bpitch + 15) / 16 * 16;
   const long long nwg = (long long)a.ntm * a.ntn * B;
   if (nwg <= 0) return BC_OK;
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
@@ -371,10 +401,14 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   a.wsc = P == 2 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
                                                   (long long)a.ntm * a.nchunks * a.K * P * t.WM * t.MT * 1024)
                  : nullptr;
-  const size_t lds = x6_lds(t, ncol, P);
+  const size_t lds = x6_lds(t, ncol, P, a.s);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
+  const size_t lds2 = x6_lds(t, ncol, P, a.s, 2);
   if (a.K == 1 && ncol == BN && x6_pw_on())
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
+  else if (P == 2 && a.K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (NT > 1 && lds2 <= 160 * 1024)))
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, (P == 2 ? 2 : 1)>), dim3(a.nwg), dim3(512),
+                       lds2, st, a);
   else
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), lds, st, a);
   BC_CHECK_LAUNCH();
@@ -407,6 +441,8 @@ int x6_launch_tile(ConvArgs& a, int B, int tile, hipStream_t st);
     case 17: return launch_x6<4, 1, 2, 4, P>(a, B, st);            \
     case 18: return launch_x6<8, 2, 2, 4, P>(a, B, st);            \
     case 19: return launch_x6<4, 4, 4, 2, P>(a, B, st);            \
+    case 20: return launch_x6<6, 4, 2, 4, P>(a, B, st);            \
+    case 21: return launch_x6<8, 4, 2, 4, P>(a, B, st);            \
   }                                                                \
   return BC_ERR_ARG;
 

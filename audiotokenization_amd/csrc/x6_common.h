@@ -18,6 +18,10 @@ typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 
 constexpr int X6_BKC = 32;            // channels per chunk = K of one bf16 MFMA
 constexpr int X6_PITCH = 80;          // bytes per column per plane (64 data + 16 pad)
+// conv1d_x6_kernel's B tile: stride-1 tiles use a 64-B pitch with the four 16-B channel groups of
+// column c XOR-swizzled by (c >> 1) & 3 (conflict-free ds_read_b128 fragment reads at any tap shift,
+// 4-way ds_write_b32 staging); strided tiles keep the padded 80-B pitch (conflict-free at stride 2).
+inline int x6_pitch(int s) { return s == 1 ? 64 : 80; }
 constexpr int X6_MAXCOL_ITERS = 11;   // 32-column passes per chunk: NCOL <= 352 (22 B loads / thread)
 
 // s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding: vmcnt[3:0] + [15:14])

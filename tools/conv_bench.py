@@ -88,7 +88,7 @@ def main():
         ms = e0.elapsed_time(e1) / a.iters
         best = min(best or (ms, cfg), (ms, cfg))
         print(f"Cin={a.cin} Cout={a.cout} k={a.k} s={a.s} d={a.d} T={Tout} B={a.B} cfg={cfg}{'*' if cfg == chosen else ''} "
-              f"({L.conv_kernel_name(cfg, a.k)}): {ms:.3f} ms  {fl / ms / 1e9:.1f} TFLOP/s  "
+              f"({L.conv_kernel_name(cfg, a.k, a.s, a.d)}): {ms:.3f} ms  {fl / ms / 1e9:.1f} TFLOP/s  "
               f"{nb / ms / 1e6:.0f} GB/s", flush=True)
     if len(cfgs) > 1 and best:
         print(f"  best cfg {best[1]} {best[0]:.3f} ms (library choice {chosen})", flush=True)
