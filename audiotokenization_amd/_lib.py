@@ -203,9 +203,22 @@ def conv_kernel_name(cfg: int, taps: int = 0, stride: int = 1, dilation: int = 1
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
 
 
-def resunit_kernel_name(cfg: int) -> str:
+def resunit_kernel_name(cfg: int, C: int = 0, dilation: int = 1) -> str:
+    """Kernel symbol of a bc_resunit_fwd launch (resunit_x6.hip launch_ru / ru_tps)."""
     mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
-    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, {2 if cfg >= 300 else 3}>"
+    if cfg < 300:
+        return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 3>"
+    forced = os.environ.get("BC_RU_TPS")
+    tps = int(forced) if forced in ("1", "2", "4") else 1
+    if forced not in ("1", "2", "4") and C:
+        bn = 16 * nt * wn
+        bplane = -(-(bn + 6 * dilation) * 64 // 16) * 16
+        ph2 = 2 * -(-C // 32) * bn * 64
+        for t in (4, 2):
+            if (t < 4 or C <= 64) and max(2 * bplane + 2 * t * 2 * wm * mt * 1024, ph2) <= 80 * 1024:
+                tps = t
+                break
+    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 2{', %d' % tps if tps > 1 else ''}>"
 
 
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6":

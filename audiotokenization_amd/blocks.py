@@ -121,7 +121,7 @@ class ResidualUnit(nn.Module):
         if tm is not None:
             flops = 2.0 * B * C * C * T * 8  # k=7 and k=1
             nbytes = 4.0 * x_act.numel() * (3 + dual)
-            tm.end(ev, L.resunit_kernel_name(cfg), flops, nbytes)
+            tm.end(ev, L.resunit_kernel_name(cfg, C, conv7.dilation), flops, nbytes)
         if next_act is None:
             return y, None
         if dual:

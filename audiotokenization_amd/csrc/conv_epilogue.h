@@ -26,9 +26,11 @@ __device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, fl
 // col0 + 16 j.
 // SC (h3 kernels): the accumulator holds x*S_x times w*S_w[co] products; acc * (a.wsc[co] * xinv)
 // (a power of two: exact) restores the fp32 dot product before the bias is added.
-template <int MT, int NT, bool SC = false>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
-                                              int col0, int lane, float xinv = 1.f) {
+// RP / rpre (MT == 1 only): the residual's 16-byte groups already loaded by the caller, one per n-tile,
+// for exactly the lanes / tiles that take the 16-byte path (conv_epilogue_res).
+template <int MT, int NT, bool SC, bool RP>
+__device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
+                                                   int col0, int lane, float xinv, const floatx4 (&rpre)[NT]) {
   float* yb = a.y + (long long)b * a.ybs;
   float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
@@ -49,7 +51,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
       if (a.vec && nb + 3 < a.Nout) {
         const long long yi = rowoff + nb;
         floatx4 r = {0.f, 0.f, 0.f, 0.f};
-        if (rb) r = *reinterpret_cast<const floatx4*>(rb + yi);
+        if (rb) r = (MT == 1 && RP) ? rpre[j] : *reinterpret_cast<const floatx4*>(rb + yi);
         floatx4 v, sv;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -90,6 +92,17 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (
       }
     }
   }
+}
+
+template <int MT, int NT, bool SC = false>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
+                                              int col0, int lane, float xinv = 1.f) {
+  conv_epilogue_impl<MT, NT, SC, false>(a, acc, b, row0, col0, lane, xinv, acc[0]);
+}
+template <int NT, bool SC = false>
+__device__ __forceinline__ void conv_epilogue_res(const ConvArgs& a, const floatx4 (&acc)[1][NT], int b, int row0,
+                                                  int col0, int lane, float xinv, const floatx4 (&rpre)[NT]) {
+  conv_epilogue_impl<1, NT, SC, true>(a, acc, b, row0, col0, lane, xinv, rpre);
 }
 
 // Host: may the epilogue use 16-byte accesses for this launch?  (unit output stride, every row

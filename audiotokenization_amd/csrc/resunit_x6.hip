@@ -18,6 +18,8 @@
 // Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
 // P = 3: x6 (3 bf16 planes, 6 products); P = 2: h3 (2 block-scaled fp16 planes, 3 products; the k=7
 // input is scaled per staged chunk as in conv1d_x6.hip, h per workgroup tile from its block maximum).
+#include <cstdlib>
+
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
@@ -33,11 +35,13 @@ struct RUExtra {
   const float* s2b;  //                               inv_beta  [C]
   int hplane;        // bytes per Hs plane = nck1 * BN * 64
   int nck1;          // 32-channel chunks of the k=1 conv's input
+  int dbg;           // BC_RU_DEBUG timing experiments (wrong results): 1 no A copies, 2 no B loads, 4 no epilogue, 8 no phase 2
 };
 
 __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
-template <int MT, int NT, int WM, int WN, int P>
+// TPS: k=7 taps per phase-1 K-step (one A copy, one wait and one barrier per TPS taps).
+template <int MT, int NT, int WM, int WN, int P, int TPS = 1>
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
   static_assert(P == 2 || P == 3, "x6 or h3 operands");
   typedef typename FragType<P>::type frag_t;
@@ -56,8 +60,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 
   const int ncol = a.win;
   const int bplane = a.bstage;
-  unsigned char* Bs = smem_ru;                 // phase 1: [P][ncol][80 B]
-  unsigned char* As = smem_ru + P * bplane;    // phase 1: [2][P][QA][1 KiB]
+  unsigned char* Bs = smem_ru;                 // phase 1: [P][ncol][64 B] (16-B groups swizzled, x6_pitch)
+  unsigned char* As = smem_ru + P * bplane;    // phase 1: [2][TPS][P][QA][1 KiB]
+  auto bgrp = [](int col, int g) { return col * 64 + 16 * (g ^ ((col >> 1) & 3)); };
   unsigned char* Hs = smem_ru;                 // phase 2: [P][nck1][BN][64 B] (aliases Bs and As)
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
@@ -80,13 +85,16 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   const int in0 = n0 - a.pl;
 
   const int K = a.K;
-  const int nsteps = a.nchunks * K;
+  const int kst = (K + TPS - 1) / TPS;  // phase-1 K-steps per chunk
+  const int nsteps = a.nchunks * kst;
   const int a_pieces = P * QA;
 
   auto issue_a = [&](const float* w, int step, int buf) {
-    const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)step * (a_pieces * 1024);
-    unsigned char* dst = As + buf * (a_pieces * 1024);
-    for (int q = wave; q < a_pieces; q += 8)
+    const int c = step / kst, t0 = (step - c * kst) * TPS;
+    const int n = (K - t0 < TPS ? K - t0 : TPS) * a_pieces;
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)(c * K + t0) * (a_pieces * 1024);
+    unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
+    for (int q = wave; q < n; q += 8)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);
   };
@@ -133,14 +141,14 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         if constexpr (P == 2) {
           unsigned h, m;
           split2_h(bv0[i] * xs, bv1[i] * xs, h, m);
-          unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+          unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
           *reinterpret_cast<unsigned*>(p) = h;
           *reinterpret_cast<unsigned*>(p + bplane) = m;
           continue;
         }
         unsigned h, m, l;
         split2(bv0[i], bv1[i], h, m, l);
-        unsigned char* p = Bs + col * X6_PITCH + bp * 4;
+        unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
         *reinterpret_cast<unsigned*>(p) = h;
         *reinterpret_cast<unsigned*>(p + bplane) = m;
         *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
@@ -156,7 +164,6 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
     for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int col_lane = wn * NT * 16 + (lane & 15);
-  const int kgrp16 = (lane >> 4) * 16;
 
   // P == 2: next chunk's scale = min(current, its block scale); the accumulator follows exactly
   auto h3_next_scale = [&](int par) {
@@ -183,19 +190,27 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   __syncthreads();
 
 
+  // phase-2 wave geometry
+  const bool p2 = wave < QA * NPW;
+  const int mq = wave % QA, jg = wave / QA;
+
   for (int c = 0; c < a.nchunks; ++c) {
-    for (int tap = 0; tap < K; ++tap) {
-      const int step = c * K + tap;
-      if (step + 1 < nsteps) issue_a(a.w, step + 1, (step + 1) & 1);
-      if (tap == 0 && c + 1 < a.nchunks) load_b(c + 1);
-      const unsigned char* Ab = As + (step & 1) * (a_pieces * 1024);
-      const unsigned char* Bcol = Bs + (col_lane + tap * a.d) * X6_PITCH + kgrp16;
+    for (int tp = 0; tp < kst; ++tp) {
+      const int step = c * kst + tp;
+      if (step + 1 < nsteps && !(r.dbg & 1)) issue_a(a.w, step + 1, (step + 1) & 1);
+      if (tp == 0 && c + 1 < a.nchunks && !(r.dbg & 2)) load_b(c + 1);
+#pragma unroll
+      for (int tt = 0; tt < TPS; ++tt) {
+      const int tap = tp * TPS + tt;
+      if (TPS > 1 && tap >= K) break;
+      const unsigned char* Ab = As + (step & 1) * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
+      const unsigned char* Bcol = Bs + bgrp(col_lane + tap * a.d, lane >> 4);
       frag_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * X6_PITCH + p * bplane);
+          bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * 64 + p * bplane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
@@ -227,13 +242,14 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         }
         }
       }
-      if (tap == K - 1 && c + 1 < a.nchunks) {
+      }
+      if (tp == kst - 1 && c + 1 < a.nchunks) {
         if constexpr (P == 2) bmax_publish((c + 1) & 1);
         lds_barrier();
         if constexpr (P == 2) h3_next_scale((c + 1) & 1);
         store_b();
       }
-      if (tap == 0 && K > 1 && c + 1 < a.nchunks)
+      if (tp == 0 && kst > 1 && c + 1 < a.nchunks)
         wait_vmcnt<2 * CI>();
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -244,8 +260,6 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   // ---------------- bridge: snake2(h + b7) -> 3 bf16 planes in LDS ----------------
   // this wave's phase-2 k=1 weight fragments (packed [chunk][plane][m-tile][lane][8]), loaded into
   // registers here so they land while the bridge runs
-  const bool p2 = wave < QA * NPW;
-  const int mq = wave % QA, jg = wave / QA;
   frag_t w1f[KC1][P];
 #pragma unroll
   for (int kc = 0; kc < KC1; ++kc)
@@ -344,7 +358,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   // ---------------- phase 2: y = conv1(h_act), input as the MFMA A operand ----------------
   // Wave (mq, jg) computes m-tile mq for n-tiles [jg * NTW, (jg + 1) * NTW) from its register-resident
   // k=1 weights; Hs is read-only here, so phase 2 runs without a barrier.
-  if (p2) {
+  if (p2 && !(r.dbg & 8)) {
     floatx4 acc2[1][NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc2[0][j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -376,10 +390,11 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         }
       }
     }
-    if constexpr (P == 2)
-      conv_epilogue<1, NTW, true>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs);
-    else
-      conv_epilogue<1, NTW>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane);
+    if (r.dbg & 4) {
+      if (acc2[0][0][0] == 1234.5f) e.y[0] = 0.f;  // keep the MFMAs alive
+    } else {
+      conv_epilogue<1, NTW, P == 2>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs);
+    }
   }
 }
 
@@ -403,13 +418,29 @@ static int ru_forced_cfg() {
   return v;
 }
 
-static size_t ru_lds(const X6Tile& t, int C, int d, int P, int* bplane, int* hplane) {
+static size_t ru_lds(const X6Tile& t, int C, int d, int P, int* bplane, int* hplane, int tps = 1) {
   const int ncol = x6_ncol(t, 7, 1, d);
-  *bplane = (ncol * X6_PITCH + 15) / 16 * 16;
+  *bplane = (ncol * 64 + 15) / 16 * 16;  // swizzled 64-B pitch (x6_common.h x6_pitch)
   *hplane = (C + X6_BKC - 1) / X6_BKC * x6_BN(t) * 64;
-  const size_t ph1 = P * (size_t)*bplane + 2 * P * (size_t)t.WM * t.MT * 1024;  // Bs + As
-  const size_t ph2 = P * (size_t)*hplane;                                         // Hs
+  const size_t ph1 = P * (size_t)*bplane + 2 * tps * P * (size_t)t.WM * t.MT * 1024;  // Bs + As
+  const size_t ph2 = P * (size_t)*hplane;                                               // Hs
   return ph1 > ph2 ? ph1 : ph2;
+}
+
+// k=7 taps per phase-1 K-step (h3), measured (profiles/r01g_ru_tps_prefetch_sweep.txt): 4 at C <= 64
+// (C = 48: -4 %), else 2 (C = 96: -2 %; 4 is 1.5x slower there), each only where the A buffers keep
+// the unit within the two-workgroups-per-CU LDS budget.  BC_RU_TPS forces 1 / 2 / 4 (timing experiments).
+static int ru_tps(const X6Tile& t, int C, int d, int P) {
+  static const int forced = [] {
+    const char* e = getenv("BC_RU_TPS");
+    return e ? atoi(e) : 0;
+  }();
+  if (P != 2) return 1;
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
+  int bp, hp;
+  for (int tps : {4, 2})
+    if ((tps < 4 || C <= 64) && ru_lds(t, C, d, P, &bp, &hp, tps) <= RU_LDS_MAX) return tps;
+  return 1;
 }
 
 // mode 1 (x6) -> cfg 1xx, mode 3 (h3) -> cfg 3xx (same tile table)
@@ -434,7 +465,8 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
   constexpr int BN = 16 * NT * WN;
   const X6Tile t{MT, NT, WM, WN};
   int bplane, hplane;
-  const size_t lds = ru_lds(t, a.Cout, a.d, P, &bplane, &hplane);
+  const int tps = ru_tps(t, a.Cout, a.d, P);
+  const size_t lds = ru_lds(t, a.Cout, a.d, P, &bplane, &hplane, tps);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   a.win = x6_ncol(t, 7, 1, a.d);
   a.bstage = bplane;
@@ -455,7 +487,12 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
     e.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(r.w1) +
                                            (long long)r.nck1 * P * QA * 1024);
   }
-  hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  if (P == 2 && tps == 4)
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P == 2 ? 4 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  else if (P == 2 && tps == 2)
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P == 2 ? 2 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  else
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
@@ -473,7 +510,11 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
   e.ybs = (long long)C * T; e.rbs = e.ybs;
   e.Cout = C; e.Nout = T; e.yT = T; e.ostride = 1; e.ooff = 0; e.epi = 0;
   e.vec = conv_epilogue_vec_ok(e);
-  RUExtra r{w1, s2a, s2b, 0, 0};
+  static const int dbg = [] {
+    const char* v = getenv("BC_RU_DEBUG");
+    return v ? atoi(v) : 0;
+  }();
+  RUExtra r{w1, s2a, s2b, 0, 0, dbg};
 #define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
   case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \
   case 300 + ID: return launch_ru<MT, NT, WM, WN, 2>(a, e, r, B, st);

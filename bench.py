@@ -78,7 +78,7 @@ def parse():
     p.add_argument("--sample-rate", type=int, default=24000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true")
-    p.add_argument("--cpu-clips", type=int, default=1)
+    p.add_argument("--cpu-clips", type=int, default=4, help="clips in the CPU-baseline sample (about 3 s each)")
     p.add_argument("--precision", choices=["fp32", "x6", "bf16", "h3"], default=None,
                    help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or h3)")
     a = p.parse_args()
