@@ -47,6 +47,7 @@ typedef __attribute__((address_space(1))) unsigned ls_gu32;
 constexpr int LS_U = 8;          // hidden units per workgroup
 constexpr int LS_WAVES = 4;
 constexpr int LS_NB = 64;        // clips per launch (4 n-tiles of 16)
+constexpr int LS_HD = 4;         // lstm_seq2: depth of the h_{t-1} register ring (k-steps)
 constexpr int LS_HSTEP_PER_UNIT = LS_NB * 3 / 2;  // floats of hseq per hidden unit per step (3 bf16 planes)
 constexpr int LS_SC1 = 16;       // buffer-op cache policy: sc1 (write-through / L1 bypass)
 constexpr unsigned LS_SPIN_LIMIT = 1u << 22;
@@ -404,7 +405,11 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         LS2_STAMP(1)
         const frag_t* hp =
             reinterpret_cast<const frag_t*>(a.hseq + ((long long)(t - 1) * 2 + h) * hhalf) + lane;
-        frag_t hbuf[2][2][P];
+        // h_{t-1} fragments through a register ring LS_HD k-steps deep: the loads of k-step ks + LS_HD - 1
+        // are issued before k-step ks's MFMAs, so L2 latency hides behind LS_HD - 1 k-steps of MFMAs
+        // (depth 2 left ~2300 of a half-step's 4600 load+MFMA cycles exposed, profiles/r01g_lstm_h3_stamps.txt)
+        constexpr int HD = LS_HD < KS ? LS_HD : KS;
+        frag_t hbuf[HD][2][P];
         auto load_ks = [&](int ks, frag_t (&dst)[2][P]) {
           const int ksa = w * KS + ks;
 #pragma unroll
@@ -412,14 +417,15 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
 #pragma unroll
             for (int p = 0; p < P; ++p) dst[nt][p] = hp[((ksa * 2 + nt) * P + p) * 64];
         };
-        load_ks(0, hbuf[0]);
+#pragma unroll
+        for (int ks = 0; ks + 1 < HD; ++ks) load_ks(ks, hbuf[ks]);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          if (ks + 1 < KS) load_ks(ks + 1, hbuf[(ks + 1) & 1]);
+          if (ks + HD - 1 < KS) load_ks(ks + HD - 1, hbuf[(ks + HD - 1) % HD]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
-            const frag_t* hb = hbuf[ks & 1][nt];
+            const frag_t* hb = hbuf[ks % HD][nt];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
               floatx4 s = acc[mt][nt];
