@@ -197,7 +197,7 @@ def conv_kernel_name(cfg: int, taps: int = 0, stride: int = 1, dilation: int = 1
     if 100 <= cfg < 400 and cfg % 100 + 100 in X6_CFGS:
         planes = {1: 3, 2: 1, 3: 2}[cfg // 100]
         mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
-        tps = ", 2" if planes == 2 and _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation) else ""
+        tps = ", 2" if planes == 2 and _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation) else ", 1"
         return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, {'true' if taps == 1 else 'false'}{tps}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"
@@ -207,7 +207,7 @@ def resunit_kernel_name(cfg: int, C: int = 0, dilation: int = 1) -> str:
     """Kernel symbol of a bc_resunit_fwd launch (resunit_x6.hip launch_ru / ru_tps)."""
     mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
     if cfg < 300:
-        return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 3>"
+        return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 3, 1>"
     forced = os.environ.get("BC_RU_TPS")
     tps = int(forced) if forced in ("1", "2", "4") else 1
     if forced not in ("1", "2", "4") and C:
@@ -218,7 +218,7 @@ def resunit_kernel_name(cfg: int, C: int = 0, dilation: int = 1) -> str:
             if (t < 4 or C <= 64) and max(2 * bplane + 2 * t * 2 * wm * mt * 1024, ph2) <= 80 * 1024:
                 tps = t
                 break
-    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 2{', %d' % tps if tps > 1 else ''}>"
+    return f"resunit_x6_kernel<{mt}, {nt}, {wm}, {wn}, 2, {tps}>"
 
 
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6":

@@ -116,7 +116,7 @@ def pmc_traffic(kernel: str):
     summary (tools/gpu_pmc.sh -> tools/pmc_summary.py -> profiles/*pmc_traffic.json), or Nones."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))  # r01_ < r01a_ < ... < r01h_
     for f in reversed(files):
         d = json.load(open(f))["kernels"].get(kernel)
         if d:
