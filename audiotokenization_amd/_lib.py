@@ -177,13 +177,13 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
                                               (8, 2, 2, 4), (4, 4, 4, 2), (6, 4, 2, 4), (8, 4, 2, 4)])}
 
 
-def _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation) -> bool:
-    """conv1d_x6_kernel.h launch_x6: does an h3 multi-tap launch run the two-taps-per-step variant?"""
-    if taps <= 1 or os.environ.get("BC_X6_TPS") == "1":
+def _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation, planes=2) -> bool:
+    """conv1d_x6_kernel.h launch_x6: does an h3 / bf16 multi-tap launch run the two-taps-per-step variant?"""
+    if taps <= 1 or planes > 2 or os.environ.get("BC_X6_TPS") == "1":
         return False
     ncol = (16 * nt * wn - 1) * stride + (taps - 1) * dilation + 1
     bplane = -(-ncol * (64 if stride == 1 else 80) // 16) * 16
-    lds2 = 2 * bplane + 2 * 2 * 2 * wm * mt * 1024
+    lds2 = planes * bplane + 2 * 2 * planes * wm * mt * 1024
     return lds2 <= 80 * 1024 or (nt > 1 and lds2 <= 160 * 1024)
 
 
@@ -197,7 +197,7 @@ def conv_kernel_name(cfg: int, taps: int = 0, stride: int = 1, dilation: int = 1
     if 100 <= cfg < 400 and cfg % 100 + 100 in X6_CFGS:
         planes = {1: 3, 2: 1, 3: 2}[cfg // 100]
         mt, nt, wm, wn = X6_CFGS[cfg % 100 + 100]
-        tps = ", 2" if planes == 2 and _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation) else ", 1"
+        tps = ", 2" if _x6_two_taps(mt, nt, wm, wn, taps, stride, dilation, planes) else ", 1"
         return f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, {'true' if taps == 1 else 'false'}{tps}>"
     mt, wm, nt, wn, bkc = CONV_CFGS[cfg]
     return f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>"

@@ -141,9 +141,9 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
-  if (planes == 2 && x6_occ_pref() == 0) {
+  if (planes <= 2 && x6_occ_pref() == 0) {  // bf16 (1 plane) follows the h3 table (measured, config 5)
     const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
-    if (c >= 0) return c + 200;  // (a phase-decomposed 1000 * s + tile keeps its phase factor)
+    if (c >= 0) return c + (planes == 2 ? 200 : 100);  // (a phase-decomposed 1000 * s + tile keeps its phase factor)
   }
   if (planes >= 2 && x6_occ_pref() == 0) {
     const int c = x6_preferred_cfg(Cout, Cin, K, s, d);

@@ -362,7 +362,7 @@ inline size_t x6_lds(const X6Tile& t, int ncol, int planes, int s, int tps = 1) 
   return planes * bplane + 2 * tps * planes * (size_t)t.WM * t.MT * 1024;
 }
 
-// h3 kernels run the multi-tap path with two taps per K-step where the doubled A buffers fit the
+// h3 and bf16 kernels run the multi-tap path with two taps per K-step where the doubled A buffers fit the
 // tile's LDS budget (measured: -4 % on the k7 convs, profiles/r01g_tps_sweep.txt); BC_X6_TPS=1 disables it.
 inline int x6_tps() {
   static const int v = [] {
@@ -406,8 +406,8 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   const size_t lds2 = x6_lds(t, ncol, P, a.s, 2);
   if (a.K == 1 && ncol == BN && x6_pw_on())
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
-  else if (P == 2 && a.K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (NT > 1 && lds2 <= 160 * 1024)))
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, (P == 2 ? 2 : 1)>), dim3(a.nwg), dim3(512),
+  else if (P <= 2 && a.K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (NT > 1 && lds2 <= 160 * 1024)))
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, (P <= 2 ? 2 : 1)>), dim3(a.nwg), dim3(512),
                        lds2, st, a);
   else
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), lds, st, a);
