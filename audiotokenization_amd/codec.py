@@ -150,6 +150,12 @@ class BigCodecDecoder(nn.Module):
         self.quantizer = self.quantizer.eval()
         return self.quantizer.get_emb()
 
+    def tokens_to_audio(self, vq):
+        """Token -> audio: codes (B, T, Nq) int64 on the device (extract_indices' (F, Nq) files, batched)
+        -> waveform (B, 1, T * hop): vq2emb (codec_decoder.py:96-99) -> transpose(1, 2) -> self(x, vq=False),
+        with the embedding written straight in the decoder's (B, D, T) layout (bc_vq2emb_ct)."""
+        return self.decode(self.quantizer.vq2emb_ct(vq))
+
     def inference_vq(self, vq):
         return self.decode(vq[None, :, :])
 

@@ -274,6 +274,12 @@ int bc_vq2emb(const long long* idx, long long idx_stride, const float* codebook,
   return vq2emb_launch(idx, idx_stride, codebook, w_out, b_out, emb, N, D, accumulate, S(stream));
 }
 
+int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const float* w_out,
+                 const float* b_out, float* emb, int B, int T, int D, int n_codes, int dim, void* stream) {
+  if (dim != 8) return BC_ERR_UNSUPPORTED;
+  return vq2emb_ct_launch(idx, nq, codebooks, w_out, b_out, emb, B, T, D, n_codes, S(stream));
+}
+
 int bc_rvq_update(float* residual, float* out, const float* q, long long n, int first,
                   void* stream) {
   if (!residual || !out || !q || n < 0) return BC_ERR_ARG;

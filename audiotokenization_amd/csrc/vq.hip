@@ -7,6 +7,7 @@
 //                               z_e + (z_q - z_e) (:68-70) -> out_proj (WN Linear 8->D, :72-74).
 //  vq_argmin_kernel           : the search alone on given projected latents z_e.
 //  vq2emb_kernel              : indices -> out_proj(codebook[idx]) (:78-91, residual_vq.py:42-48).
+//  vq2emb_ct_kernel           : the token -> audio entry: stacked quantizers, (B, D, T) output.
 //
 // Bit-exactness contract (tests/test_vq_*): given the same z_e, the indices equal the reference's.
 // The fp32 operation order below restates what torch's CPU kernels do for these shapes, verified
@@ -188,6 +189,63 @@ __global__ void vq2emb_kernel(const long long* __restrict__ idx, long long idx_s
     }
     emb[e] = accumulate ? emb[e] + v : v;
   }
+}
+
+// Token -> audio entry (codec_decoder.py:96-99 -> residual_vq.py:42-48 -> factorized_vector_quantize.py:78-81,
+// then the caller's transpose(1, 2)): idx[B][T][Nq] -> emb[B][D][T], the decoder's input layout, so the
+// transpose costs nothing.  Per quantizer q: v = (fma chain over k of w_out_q[d][k] * cb_q[idx][k] from 0) +
+// b_out_q[d], exactly vq2emb_kernel's order; the sum over quantizers starts from 0. as the reference's
+// `quantized_out = 0.` does.  Parameters of the Nq quantizers are stacked: cb [Nq][n_codes][8],
+// w_out [Nq][D][8], b_out [Nq][D].  An index outside [0, n_codes) yields NaN for its column (no
+// out-of-range read).  Thread = one position t; the workgroup walks VQ_CT_D channels, so the
+// stores are coalesced along t and the weights are wave-uniform (scalar loads).
+constexpr int VQ_CT_D = 32;
+constexpr int VQ_CT_MAXQ = 8;
+__global__ void __launch_bounds__(256) vq2emb_ct_kernel(const long long* __restrict__ idx, int nq,
+                                                        const float* __restrict__ cb, const float* __restrict__ w_out,
+                                                        const float* __restrict__ b_out, float* __restrict__ emb,
+                                                        int T, int D, int n_codes) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int d0 = blockIdx.y * VQ_CT_D;
+  const int b = blockIdx.z;
+  if (t >= T) return;
+  float c[VQ_CT_MAXQ][VQ_DIM];
+  bool bad = false;
+  for (int q = 0; q < nq; ++q) {
+    const long long k = idx[((long long)b * T + t) * nq + q];
+    const bool ok = k >= 0 && k < n_codes;
+    bad = bad || !ok;
+    const float* row = cb + ((long long)q * n_codes + (ok ? k : 0)) * VQ_DIM;
+#pragma unroll
+    for (int j = 0; j < VQ_DIM; ++j) c[q][j] = row[j];
+  }
+  float* out = emb + ((long long)b * D + d0) * T + t;
+  const int dn = D - d0 < VQ_CT_D ? D - d0 : VQ_CT_D;
+  for (int dd = 0; dd < dn; ++dd) {
+    const int d = d0 + dd;
+    float sum = 0.f;
+    for (int q = 0; q < nq; ++q) {
+      const float* w = w_out + ((long long)q * D + d) * VQ_DIM;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < VQ_DIM; ++j) acc = fmaf(w[j], c[q][j], acc);
+      sum = sum + (acc + b_out[(long long)q * D + d]);
+    }
+    out[(long long)dd * T] = bad ? __builtin_nanf("") : sum;
+  }
+}
+
+int vq2emb_ct_launch(const long long* idx, int nq, const float* cb, const float* w_out, const float* b_out,
+                     float* emb, int B, int T, int D, int n_codes, hipStream_t st) {
+  if (nq < 1 || nq > VQ_CT_MAXQ || B < 0 || T < 0 || D < 1 || n_codes < 1 || !idx || !cb || !w_out || !b_out ||
+      !emb)
+    return BC_ERR_ARG;
+  if (B == 0 || T == 0) return BC_OK;
+  if (B > 65535 || (D + VQ_CT_D - 1) / VQ_CT_D > 65535) return BC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(vq2emb_ct_kernel, dim3((T + 255) / 256, (D + VQ_CT_D - 1) / VQ_CT_D, B), dim3(256), 0, st,
+                     idx, nq, cb, w_out, b_out, emb, T, D, n_codes);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
 }
 
 // ResidualVQ bookkeeping (residual_vq.py:31-33): residual -= q; out += q

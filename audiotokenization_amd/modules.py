@@ -438,6 +438,40 @@ class ResidualVQ(nn.Module):
     def get_emb(self):
         return [layer.get_emb() for layer in self.layers]
 
+    def prepared_stack(self, device):
+        """The quantizers' codebooks, folded out_proj weights and biases stacked for bc_vq2emb_ct
+        ([Nq][n_codes][8], [Nq][D][8], [Nq][D]); built once per device and parameter version."""
+        preps = [layer.prepared(device) for layer in self.layers]
+        if len({layer.codebook_size for layer in self.layers}) != 1:
+            raise NotImplementedError("bc_vq2emb_ct stacks equal-size codebooks")
+        key = tuple(id(t) for p in preps for t in (p[0], p[5], p[6]))
+        cached = getattr(self, "_stack_cache", None)
+        if cached is None or cached[0] != key:
+            cb = torch.stack([p[0] for p in preps]).contiguous()
+            w = torch.stack([p[5] for p in preps]).contiguous()
+            bb = torch.stack([p[6] for p in preps]).contiguous()
+            self._stack_cache = (key, (cb, w, bb))
+        return self._stack_cache[1]
+
+    def vq2emb_ct(self, vq):
+        """Token -> decoder input in one launch: vq (B, T, Nq) int64 on the device -> (B, D, T) =
+        self.vq2emb(vq).transpose(1, 2) (residual_vq.py:42-48 + the caller's transpose before
+        codec_decoder.py decoder(x, vq=False)); Nq may be less than num_quantizers, as in vq2emb."""
+        if not vq.is_cuda:
+            raise L.BigCodecLibraryError("vq2emb_ct takes device index tensors")
+        if vq.dtype != torch.int64 or vq.dim() != 3:
+            raise TypeError("indices must be an int64 (B, T, num_quantizers) tensor")
+        vq = vq.contiguous()
+        B, T, nq = vq.shape
+        if not 1 <= nq <= len(self.layers):
+            raise ValueError(f"{nq} quantizer columns for a {len(self.layers)}-quantizer ResidualVQ")
+        cb, w, bb = self.prepared_stack(vq.device)
+        D = w.shape[1]
+        out = torch.empty((B, D, T), device=vq.device, dtype=torch.float32)
+        L.call("bc_vq2emb_ct", vq.data_ptr(), nq, cb.data_ptr(), w.data_ptr(), bb.data_ptr(), out.data_ptr(),
+               B, T, D, cb.shape[1], cb.shape[2], L.stream_of(vq))
+        return out
+
 
 def _vq2emb_into_strided(self, vq, i, nq, out, proj, accumulate):
     """vq: contiguous (..., nq) int64; uses column i (element stride nq)."""

@@ -34,6 +34,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "audio-sec encoded/sec/GPU (24 kHz mono, 10 s clips) + VQ index bit-exactness"
 METRIC_RT = "audio-sec encoded+quantised+decoded/sec (24 kHz mono, 10 s clips)"
+METRIC_DEC = "audio-sec decoded from tokens/sec/GPU (24 kHz mono, 10 s clips)"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec); 155 measured
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 H3_PRODUCTS = 3  # csrc/conv1d_x6.hip P = 2: three fp16 MFMAs per product term
@@ -46,6 +47,9 @@ CONFIGS = {
     4: dict(batch=64, seconds=10.0, precision=None,
             work="corpus streaming: on-device clip synthesis + encode+VQ + index all-gather + int16 host copy"),
     5: dict(batch=32, seconds=30.0, precision="bf16", work="encode+VQ, bf16 conv products"),
+    6: dict(batch=64, seconds=10.0, precision=None,
+            work="token -> audio: (B, F, 1) int64 codes resident in HBM -> bc_vq2emb_ct -> decoder "
+                 "(tokens.py service path, SURVEY 8(f) rank 3)"),
 }
 
 
@@ -174,6 +178,32 @@ def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
             torch.cat(codes, dim=1), torch.cat(wavs, dim=0) if roundtrip else None)
 
 
+def cpu_decode_baseline(codes, sds, dk, n_clips):
+    """The CPU oracle's token -> audio decode (vq2emb -> transpose -> decoder) on this host, B = 1 per
+    clip, warm.  Returns (baseline dict, waveforms)."""
+    import numpy as np
+    import torch
+
+    from oracle import bigcodec_oracle as O
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    torch.set_num_threads(threads)
+    nq = codes.shape[2]
+    with torch.no_grad():
+        O.decoder_forward(O.vq2emb(codes[:1, :20], sds[1], "quantizer.", nq).transpose(1, 2).contiguous(), sds[1], dk)
+        wavs = []
+        t0 = time.perf_counter()
+        for i in range(n_clips):
+            emb = O.vq2emb(codes[i:i + 1], sds[1], "quantizer.", nq)
+            wavs.append(O.decoder_forward(emb.transpose(1, 2).contiguous(), sds[1], dk))
+        dt = time.perf_counter() - t0
+    audio_s = n_clips * codes.shape[1] * int(np.prod(dk["up_ratios"])) / 24000.0
+    return (dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port",
+                 sample=f"{n_clips} clip(s) x {codes.shape[1]} frames, token -> audio decode, B=1, torch CPU "
+                        f"oracle, {dt:.1f} s"),
+            torch.cat(wavs, dim=0))
+
+
 def main():
     args = parse()
     import numpy as np
@@ -201,8 +231,18 @@ def main():
     cfgn = args.config
     x = synth_batch(B, n_samples, clip0=rank * B, device=dev)  # resident in HBM before timing
     state = {"batch": 0, "wav": None, "host": None}
+    tok = None
+    if cfgn == 6:  # synthetic codes of the clips' frame count, uniform over the codebook, seeded per rank
+        n_frames = n_samples // int(dec.hop_length)
+        g = torch.Generator().manual_seed(1234 + rank)
+        tok = torch.randint(0, dec.quantizer.layers[0].codebook_size, (B, n_frames, 1), generator=g)
+        tok_dev = tok.to(dev)
 
     def step():
+        if cfgn == 6:
+            with torch.no_grad():
+                state["wav"] = dec.tokens_to_audio(tok_dev)
+            return None
         with torch.no_grad():
             xb = x
             if cfgn == 4:  # the rank's next batch of the corpus, synthesised on the device
@@ -283,7 +323,14 @@ def main():
         parity = {"reference": "same batch through the fp32-accurate (x6) path", "frames": int(ref.numel()),
                   "index_mismatches": int((got != ref).sum()),
                   "mismatch_rate": round(float((got != ref).float().mean()), 5)}
-    if rank == 0 and not args.no_cpu_baseline and cfgn != 5:
+    if rank == 0 and not args.no_cpu_baseline and cfgn == 6:
+        cpu, wav_ref = cpu_decode_baseline(tok, sds, dk, args.cpu_clips)
+        w = state["wav"][: args.cpu_clips].double().cpu()
+        r = wav_ref.double()
+        parity = {"clips_checked": args.cpu_clips, "samples": int(r.numel()),
+                  "waveform_mse": float(((w - r) ** 2).mean()), "waveform_max_abs": float((w - r).abs().max()),
+                  "note": "same codes through the CPU oracle's vq2emb + decoder"}
+    if rank == 0 and not args.no_cpu_baseline and cfgn not in (5, 6):
         cpu, codes_ref, wav_ref = cpu_baseline(args.model, n_samples, sds, ek, dk, args.cpu_clips,
                                                roundtrip=cfgn == 3)
         got = codes[0] if world > 1 else codes
@@ -306,7 +353,8 @@ def main():
         if cfgn == 4 and state["host"] is not None:
             assert state["host"].dtype == np.int16
         line = {
-            "metric": METRIC_RT if cfgn == 3 else METRIC, "value": round(value, 2), "unit": "audio-sec/s",
+            "metric": METRIC_RT if cfgn == 3 else METRIC_DEC if cfgn == 6 else METRIC, "value": round(value, 2),
+            "unit": "audio-sec/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",

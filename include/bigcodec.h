@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 3
+#define BC_ABI_VERSION 4
 
 int bc_abi_version(void);
 
@@ -155,6 +155,13 @@ int bc_vq2emb(const long long* idx, long long idx_stride, const float* codebook,
               int dim, int accumulate, void* stream);
 int bc_rvq_update(float* residual, float* out, const float* q, long long n, int first,
                   void* stream);
+/* bc_vq2emb_ct: the token -> audio entry (codec_decoder.py:96-99 vq2emb, then the caller's
+ *   transpose(1, 2) before decoder(x, vq=False)): idx[B][T][nq] int64 -> emb[B][D][T], summed over the
+ *   nq quantizers in the reference's order.  Quantizer parameters stacked: codebooks [nq][n_codes][dim],
+ *   w_out [nq][D][dim] (folded weight norm), b_out [nq][D].  1 <= nq <= 8, dim == 8.  An index outside
+ *   [0, n_codes) gives NaN in its column (never an out-of-range read). */
+int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const float* w_out,
+                 const float* b_out, float* emb, int B, int T, int D, int n_codes, int dim, void* stream);
 
 /* ---- Layout helpers & synthetic input --------------------------------------------------------
  * bc_btc_to_ctb: x[B][C][T] -> y[C][T][B];  bc_ctb_to_btc_add: out = transpose(y) + skip.

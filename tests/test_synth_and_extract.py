@@ -83,3 +83,27 @@ def test_shard_range_partitions(n, w):
         assert hi - lo in (n // w, n // w + 1)
     assert seen == list(range(n))
     assert batches(0, 10, 4) == [(0, 4), (4, 8), (8, 10)]
+
+
+def test_token_files_host_side(tmp_path):
+    """tokens.py host logic (no GPU): extract.save_indices files load back, stack ragged with padding and
+    lengths, int16 codes >= 32768 wrap back, out-of-range codes and mixed quantizer counts raise."""
+    import pytest
+
+    from audiotokenization_amd import extract, tokens
+
+    a = np.array([[0], [5], [8191]], dtype=np.int16)
+    b = np.array([[3], [4]], dtype=np.int16)
+    pa = extract.save_indices(str(tmp_path), "dev-clean", "1-2-0003", a)
+    pb = extract.save_indices(str(tmp_path), "dev-clean", "1-2-0004", b)
+    la, lb = tokens.load_indices(pa), tokens.load_indices(pb)
+    assert la.dtype == np.int16 and np.array_equal(la, a)
+    codes, lengths = tokens.codes_to_device([la, lb], "cpu", 8192)
+    assert lengths == [3, 2] and codes.dtype == torch.int64 and codes.shape == (2, 3, 1)
+    assert codes[:, :, 0].tolist() == [[0, 5, 8191], [3, 4, 0]]
+    big = np.array([[40000 - 65536]], dtype=np.int16)  # a 65536-entry codebook's index 40000, as int16
+    assert tokens.codes_to_device([big], "cpu", 65536)[0].item() == 40000
+    with pytest.raises(ValueError):
+        tokens.codes_to_device([np.array([[8192]], dtype=np.int16)], "cpu", 8192)
+    with pytest.raises(ValueError):
+        tokens.codes_to_device([a, np.zeros((2, 2), dtype=np.int16)], "cpu", 8192)
