@@ -43,6 +43,7 @@ _SIGS = {
     "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
     "bc_vq2emb": (I, [P, L, P, P, P, P, L, I, I, I, I, P]),
     "bc_vq2emb_ct": (I, [P, I, P, P, P, P, I, I, I, I, I, P]),
+    "bc_resample_sinc": (I, [P, P, P, I, L, L, L, I, I, I, I, P]),
     "bc_rvq_update": (I, [P, P, P, L, I, P]),
     "bc_btc_to_ctb": (I, [P, P, I, I, I, P]),
     "bc_ctb_to_btc_add": (I, [P, P, P, I, I, I, P]),

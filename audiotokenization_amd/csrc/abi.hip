@@ -280,6 +280,11 @@ int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const flo
   return vq2emb_ct_launch(idx, nq, codebooks, w_out, b_out, emb, B, T, D, n_codes, S(stream));
 }
 
+int bc_resample_sinc(const float* x, float* y, const float* kern, int B, long long Lin, long long Lout,
+                     long long y_pitch, int orig, int new_freq, int taps, int width, void* stream) {
+  return resample_sinc_launch(x, y, kern, B, Lin, Lout, y_pitch, orig, new_freq, taps, width, S(stream));
+}
+
 int bc_rvq_update(float* residual, float* out, const float* q, long long n, int first,
                   void* stream) {
   if (!residual || !out || !q || n < 0) return BC_ERR_ARG;

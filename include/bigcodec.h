@@ -163,6 +163,15 @@ int bc_rvq_update(float* residual, float* out, const float* q, long long n, int 
 int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const float* w_out,
                  const float* b_out, float* emb, int B, int T, int D, int n_codes, int dim, void* stream);
 
+/* ---- Real-audio ingest ------------------------------------------------------------------------
+ * bc_resample_sinc: torchaudio.transforms.Resample(orig, new) as extract_indices.py:129-132 and
+ *   data_module.py:95-98 call it: x[B][Lin] -> y[b * y_pitch + o], o < Lout = ceil(new * Lin / orig)
+ *   (y_pitch >= Lout leaves room for extract_indices.py:135-137's pad_to_stride zeros), with
+ *   orig / new already divided by their gcd and kern[new][taps] the host-built sinc-Hann filters
+ *   (audiotokenization_amd/ingest.py sinc_resample_kernel, taps = 2 * width + orig). */
+int bc_resample_sinc(const float* x, float* y, const float* kern, int B, long long Lin, long long Lout,
+                     long long y_pitch, int orig, int new_freq, int taps, int width, void* stream);
+
 /* ---- Layout helpers & synthetic input --------------------------------------------------------
  * bc_btc_to_ctb: x[B][C][T] -> y[C][T][B];  bc_ctb_to_btc_add: out = transpose(y) + skip.
  * bc_synth_clips: x[B][T] white noise, clip i = clip0 + b (SURVEY.md §8(d) spec). */
