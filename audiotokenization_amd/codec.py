@@ -12,7 +12,7 @@ import torch.nn as nn
 
 from .blocks import DecoderBlock, EncoderBlock, ResLSTM, produce_conv
 from .conv import WNConv1d
-from .modules import Activation1d, ResidualVQ, SnakeBeta, _as_input
+from .modules import FSQ, Activation1d, ResidualVQ, SnakeBeta, _as_input, _zeros
 
 
 class _Tanh(nn.Module):
@@ -91,12 +91,14 @@ class BigCodecDecoder(nn.Module):
         self.ngf = ngf
         self.up_ratios = up_ratios
         self.fsq = fsq
-        if fsq:
-            raise NotImplementedError("FSQ quantizer (fsq=True) is a SURVEY §8(f) 'next' item; no shipped "
-                                      "config enables it")
-        self.quantizer = ResidualVQ(num_quantizers=vq_num_quantizers, dim=in_channels, codebook_size=codebook_size,
-                                    codebook_dim=codebook_dim, threshold_ema_dead_code=2, commitment=vq_commit_weight,
-                                    weight_init=vq_weight_init, full_commit_loss=vq_full_commit_loss)
+        if fsq:  # codec_decoder.py:41-47
+            self.quantizer = FSQ(levels=fsq_levels, channel_first=True, dim=in_channels)
+            assert codebook_size == np.prod(fsq_levels), "codebook_size must be equal to the product of fsq_levels"
+        else:
+            self.quantizer = ResidualVQ(num_quantizers=vq_num_quantizers, dim=in_channels,
+                                        codebook_size=codebook_size, codebook_dim=codebook_dim,
+                                        threshold_ema_dead_code=2, commitment=vq_commit_weight,
+                                        weight_init=vq_weight_init, full_commit_loss=vq_full_commit_loss)
         channels = upsample_initial_channel
         layers = [WNConv1d(in_channels, channels, kernel_size=7, padding=3, causal=causal)]
         if use_rnn:
@@ -139,6 +141,9 @@ class BigCodecDecoder(nn.Module):
 
     def forward(self, x, vq=True):
         if vq is True:
+            if self.fsq:  # codec_decoder.py:87-89
+                x, q = self.quantizer(x)
+                return x, q, _zeros(x.shape[0], x.device)
             return self.quantizer(x)
         return self.decode(x)
 

@@ -8,6 +8,7 @@
 //  vq_argmin_kernel           : the search alone on given projected latents z_e.
 //  vq2emb_kernel              : indices -> out_proj(codebook[idx]) (:78-91, residual_vq.py:42-48).
 //  vq2emb_ct_kernel           : the token -> audio entry: stacked quantizers, (B, D, T) output.
+//  fsq_fwd_kernel             : the FSQ quantizer (fsq=True decoders).
 //
 // Bit-exactness contract (tests/test_vq_*): given the same z_e, the indices equal the reference's.
 // The fp32 operation order below restates what torch's CPU kernels do for these shapes, verified
@@ -189,6 +190,80 @@ __global__ void vq2emb_kernel(const long long* __restrict__ idx, long long idx_s
     }
     emb[e] = accumulate ? emb[e] + v : v;
   }
+}
+
+// FSQ quantizer (decoder fsq=True, codec_decoder.py:41-47, 85-92 -> the vendored lucidrains
+// finite_scalar_quantization.py FSQ.forward, eval, channel_first, one codebook).  One thread per frame:
+//   zi[j]   = project_in: fma chain over the D channels from 0, + bias[j]        (nn.Linear D -> d)
+//   b[j]    = tanh(zi[j] + shift[j]) * half_l[j] - offset[j]                        (bound, :118-123)
+//   q[j]    = b[j] + (rint(b[j]) - b[j])                  (round_ste's forward value; rint = half to even)
+//   code[j] = q[j] / half_width[j]                                                  (quantize, :147-149)
+//   idx     = int( sum_j (code[j] * half_width[j] + half_width[j]) * basis[j] )     (codes_to_indices)
+//   post[b][c][t] = fma chain over j of w_out[c][j] * code[j] from 0, + b_out[c]   (project_out)
+// The per-level constants are computed on the host with the reference's own float32 torch expressions
+// (modules.FSQ.constants) and passed as consts[5][d] = half_l, offset, shift, half_width, basis.
+constexpr int FSQ_MAXD = 8;
+__global__ void __launch_bounds__(256) fsq_fwd_kernel(const float* __restrict__ z, const float* __restrict__ w_in,
+                                                      const float* __restrict__ b_in, const float* __restrict__ w_out,
+                                                      const float* __restrict__ b_out, const float* __restrict__ consts,
+                                                      int* __restrict__ idx, float* __restrict__ post, int B, int D,
+                                                      int T, int nd) {
+  const long long NF = (long long)B * T;
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= NF) return;
+  const int b = (int)(n / T), t = (int)(n % T);
+  const float* zb = z + (long long)b * D * T + t;
+  float zi[FSQ_MAXD];
+#pragma unroll
+  for (int j = 0; j < FSQ_MAXD; ++j) zi[j] = 0.f;
+  for (int c = 0; c < D; ++c) {
+    const float zv = zb[(long long)c * T];
+#pragma unroll
+    for (int j = 0; j < FSQ_MAXD; ++j)
+      if (j < nd) zi[j] = fmaf(w_in[j * D + c], zv, zi[j]);
+  }
+  float code[FSQ_MAXD];
+  float isum = 0.f;
+#pragma unroll
+  for (int j = 0; j < FSQ_MAXD; ++j) {
+    if (j >= nd) {
+      code[j] = 0.f;
+      continue;
+    }
+    const float half_l = consts[j], offset = consts[nd + j], shift = consts[2 * nd + j];
+    const float hw = consts[3 * nd + j], basis = consts[4 * nd + j];
+    const float v = zi[j] + b_in[j];
+    const float bd = tanhf(v + shift) * half_l - offset;
+    const float q = bd + (rintf(bd) - bd);
+    code[j] = q / hw;
+    isum = isum + (code[j] * hw + hw) * basis;
+  }
+  idx[n] = (int)isum;
+  if (post) {
+    float* pb = post + (long long)b * D * T + t;
+    for (int c = 0; c < D; ++c) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < FSQ_MAXD; ++j)
+        if (j < nd) acc = fmaf(w_out[c * nd + j], code[j], acc);
+      pb[(long long)c * T] = acc + b_out[c];
+    }
+  }
+}
+
+int fsq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* w_out, const float* b_out,
+                   const float* consts, int* idx, float* post, int B, int D, int T, int nd, hipStream_t st) {
+  if (!z || !w_in || !b_in || !consts || !idx || B < 0 || D < 1 || T < 0 || nd < 1) return BC_ERR_ARG;
+  if ((post != nullptr) != (w_out != nullptr) || (w_out != nullptr) != (b_out != nullptr)) return BC_ERR_ARG;
+  if (nd > FSQ_MAXD) return BC_ERR_UNSUPPORTED;
+  const long long NF = (long long)B * T;
+  if (NF == 0) return BC_OK;
+  const long long nwg = (NF + 255) / 256;
+  if (nwg > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(fsq_fwd_kernel, dim3((unsigned)nwg), dim3(256), 0, st, z, w_in, b_in, w_out, b_out, consts, idx,
+                     post, B, D, T, nd);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
 }
 
 // Token -> audio entry (codec_decoder.py:96-99 -> residual_vq.py:42-48 -> factorized_vector_quantize.py:78-81,

@@ -490,3 +490,67 @@ def _vq2emb_into_strided(self, vq, i, nq, out, proj, accumulate):
 
 
 FactorizedVectorQuantize._vq2emb_into_strided = _vq2emb_into_strided
+
+
+class FSQ(nn.Module):
+    """The vendored lucidrains FSQ (vq/vector_quantize_pytorch_lucidrains/finite_scalar_quantization.py:
+    55-262) as BigCodecDecoder builds it for fsq=True (codec_decoder.py:41-47: levels, channel_first=True,
+    dim=in_channels; one codebook, nn.Linear projections with bias; the same state_dict keys
+    project_in.weight/bias, project_out.weight/bias).  Eval forward: one bc_fsq_fwd launch,
+    z (B, D, T) -> (project_out(codes) (B, D, T), indices (B, T) int32)."""
+
+    def __init__(self, levels, dim=None, num_codebooks=1, channel_first=False, projection_has_bias=True, **_):
+        super().__init__()
+        if num_codebooks != 1 or not projection_has_bias:
+            raise NotImplementedError("FSQ: one codebook with biased projections (the decoder's use)")
+        self.levels = [int(v) for v in levels]
+        if not 1 <= len(self.levels) <= 8:
+            raise NotImplementedError("FSQ: 1..8 levels")
+        self.codebook_dim = len(self.levels)
+        self.dim = dim if dim is not None else self.codebook_dim
+        self.channel_first = channel_first
+        self.codebook_size = int(np.prod(self.levels))
+        self.has_projections = self.dim != self.codebook_dim
+        self.project_in = nn.Linear(self.dim, self.codebook_dim) if self.has_projections else nn.Identity()
+        self.project_out = nn.Linear(self.codebook_dim, self.dim) if self.has_projections else nn.Identity()
+        self._cache = _DeviceCache()
+
+    def constants(self) -> torch.Tensor:
+        """[5][d] float32 = half_l, offset, shift, half_width, basis, from the reference's own torch
+        expressions (bound :118-123, quantize :147-149, codes_to_indices :164-168), on the CPU."""
+        lv = torch.tensor(self.levels, dtype=torch.int32)
+        half_l = (lv - 1) * (1 + 1e-3) / 2
+        offset = torch.where(lv % 2 == 0, 0.5, 0.0)
+        shift = (offset / half_l).atanh()
+        hw = lv // 2
+        basis = torch.cumprod(torch.tensor([1] + self.levels[:-1]), dim=0, dtype=torch.int32)
+        return torch.stack([half_l.float(), offset.float(), shift.float(), hw.float(), basis.float()]).contiguous()
+
+    def prepared(self, device):
+        lin_in, lin_out = self.project_in, self.project_out
+        src = [lin_in.weight, lin_in.bias, lin_out.weight, lin_out.bias] if self.has_projections else []
+
+        def build():
+            if self.has_projections:
+                w_in, b_in, w_out, b_out = (_cpu(t).contiguous() for t in src)
+            else:  # identity projections: exact through the fma chains (x * 1 + 0)
+                w_in = w_out = torch.eye(self.dim)
+                b_in = b_out = torch.zeros(self.dim)
+            return tuple(t.to(device) for t in (w_in, b_in, w_out, b_out, self.constants()))
+        return self._cache.get(_pkey(*src) + (str(device),), build)
+
+    def forward(self, z):
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("training-mode FSQ is out of scope of the HIP inference path; call .eval()")
+        if not self.channel_first:
+            raise NotImplementedError("FSQ on the HIP path takes channel-first (B, D, T) input, as the decoder uses it")
+        z = _as_input(z)
+        B, D, T = z.shape
+        if D != self.dim:
+            raise ValueError(f"expected dimension of {self.dim} but found dimension of {D}")
+        w_in, b_in, w_out, b_out, consts = self.prepared(z.device)
+        idx = torch.empty((B, T), device=z.device, dtype=torch.int32)
+        post = torch.empty_like(z)
+        L.call("bc_fsq_fwd", z.data_ptr(), w_in.data_ptr(), b_in.data_ptr(), w_out.data_ptr(), b_out.data_ptr(),
+               consts.data_ptr(), idx.data_ptr(), post.data_ptr(), B, D, T, self.codebook_dim, L.stream_of(z))
+        return post, idx

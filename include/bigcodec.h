@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 4
+#define BC_ABI_VERSION 5
 
 int bc_abi_version(void);
 
@@ -162,6 +162,14 @@ int bc_rvq_update(float* residual, float* out, const float* q, long long n, int 
  *   [0, n_codes) gives NaN in its column (never an out-of-range read). */
 int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const float* w_out,
                  const float* b_out, float* emb, int B, int T, int D, int n_codes, int dim, void* stream);
+
+/* bc_fsq_fwd: FSQ.forward (vendored lucidrains finite_scalar_quantization.py:205-262; the decoder's
+ *   fsq=True quantizer, codec_decoder.py:41-47, 85-92), eval, channel_first: z[B][D][T] ->
+ *   idx[B][T] int32 and (optional) post[B][D][T] = project_out(codes).  w_in [d][D], b_in [d], w_out [D][d],
+ *   b_out [D]; consts[5][d] = half_l, offset, shift, half_width, basis (float32, from the reference's own
+ *   expressions); 1 <= d <= 8. */
+int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float* w_out, const float* b_out,
+               const float* consts, int* idx, float* post, int B, int D, int T, int d, void* stream);
 
 /* ---- Real-audio ingest ------------------------------------------------------------------------
  * bc_resample_sinc: torchaudio.transforms.Resample(orig, new) as extract_indices.py:129-132 and

@@ -12,6 +12,7 @@ with the reference's own key names:
   decoder_forward   vq/codec_decoder.py:59-94 (vq=False path)
   rvq_forward       vq/residual_vq.py:21-40 + vq/factorized_vector_quantize.py:29-76, 93-108
   vq2emb            vq/residual_vq.py:42-48 + vq/factorized_vector_quantize.py:78-91
+  fsq_forward       vq/vector_quantize_pytorch_lucidrains/finite_scalar_quantization.py:205-262 (fsq=True)
 
 Pinning: tests/test_oracle_pinned.py checks this restatement bit-for-bit (torch.equal) against the
 reference modules imported from /root/reference (in the development container only) and against
@@ -254,6 +255,30 @@ def vq2emb(vq: Tensor, sd: SD, prefix: str = "quantizer.", num_quantizers: int =
             emb = _linear(emb, sd, p + "out_proj.")
         out = out + emb
     return out
+
+
+def fsq_forward(z: Tensor, sd: SD, levels: Sequence[int], prefix: str = "quantizer."):
+    """FSQ.forward (vq/vector_quantize_pytorch_lucidrains/finite_scalar_quantization.py:205-262) as the
+    fsq=True decoder calls it (codec_decoder.py:41-47, 87-88): eval, channel_first, one codebook,
+    projections with bias.  z (B, D, T) -> (out (B, D, T), indices (B, T) int32)."""
+    lv = torch.tensor(list(levels), dtype=torch.int32)
+    basis = torch.cumprod(torch.tensor([1] + list(levels[:-1])), dim=0, dtype=torch.int32)
+    x = z.transpose(1, 2)  # rearrange b d ... -> b ... d (pack_one is a no-op for 3-D input)
+    if (prefix + "project_in.weight") in sd:
+        x = F.linear(x, sd[prefix + "project_in.weight"], sd[prefix + "project_in.bias"])
+    x = x[:, :, None, :]  # b n (c d) -> b n c d, c = 1
+    half_l = (lv - 1) * (1 + 1e-3) / 2  # bound (:118-123)
+    offset = torch.where(lv % 2 == 0, 0.5, 0.0)
+    shift = (offset / half_l).atanh()
+    bounded = (x + shift).tanh() * half_l - offset
+    quantized = bounded + (bounded.round() - bounded)  # round_ste forward value (:49-52)
+    half_width = lv // 2
+    codes = quantized / half_width  # quantize (:147-149)
+    indices = ((codes * half_width + half_width) * basis).sum(dim=-1).to(torch.int32)  # codes_to_indices
+    codes = codes.reshape(codes.shape[0], codes.shape[1], -1)
+    if (prefix + "project_out.weight") in sd:
+        codes = F.linear(codes, sd[prefix + "project_out.weight"], sd[prefix + "project_out.bias"])
+    return codes.transpose(1, 2), indices[..., 0]
 
 
 def strip_prefix(sd: Mapping[str, Tensor], prefix: str) -> Dict[str, Tensor]:

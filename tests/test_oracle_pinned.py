@@ -92,3 +92,27 @@ def test_c_oracle_on_model_latents(golden):
         ze = g["z_e"]  # (B, 8, F)
         idx = vq_c.argmin(ze.transpose(0, 2, 1).reshape(-1, 8), dsd["quantizer.layers.0._codebook.weight"])
         assert np.array_equal(idx, g["codes"][0].reshape(-1)), fname
+
+
+FSQ_FILES = sorted(f for f in os.listdir(GOLDEN) if f.startswith("fsq_"))
+
+
+@pytest.mark.parametrize("fname", FSQ_FILES)
+def test_fsq_fixture(golden, fname):
+    """The FSQ restatement (fsq=True decoders) reproduces the reference's vendored lucidrains FSQ bit for bit
+    (tools/make_golden_fsq.py), and the decoder restatement its waveform."""
+    from helpers import build_models
+
+    g = golden(fname)
+    meta = g["meta"]
+    _, dec, _, dsd, _, dk = build_models(meta["model"], **meta["overrides"])
+    assert sorted(k for k in dec.state_dict() if k.startswith("quantizer.")) == \
+        ["quantizer.project_in.bias", "quantizer.project_in.weight", "quantizer.project_out.bias",
+         "quantizer.project_out.weight"]
+    sd = torch_sd(dsd)
+    with torch.no_grad():
+        post, idx = O.fsq_forward(torch.from_numpy(g["z"]), sd, meta["levels"])
+        wav = O.decoder_forward(post, sd, dk)
+    assert idx.dtype == torch.int32 and torch.equal(idx, torch.from_numpy(g["codes"]))
+    assert torch.equal(post, torch.from_numpy(g["post"]))
+    assert torch.equal(wav, torch.from_numpy(g["wav"]))
