@@ -38,6 +38,7 @@ _SIGS = {
     "bc_mfma_probe": (I, [P, I, I, P]),
     "bc_lstm_workspace_floats": (L, [I, I, I]),
     "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
+    "bc_reslstm_fwd_state": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P, P, P, P, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
     "bc_vq_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P]),
     "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
@@ -51,7 +52,7 @@ _SIGS = {
     "bc_synth_clips": (I, [P, I, L, L, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 5  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 6  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

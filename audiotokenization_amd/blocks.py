@@ -267,7 +267,9 @@ class ResLSTM(nn.Module):
         self.lstm = LSTM(dimension, dimension if not bidirectional else dimension // 2, num_layers,
                          batch_first=True, bidirectional=bidirectional)
 
-    def run(self, x, out_snake=None):
+    def run(self, x, out_snake=None, state=None):
+        """state (streaming): None, or ((h0, c0) or None, (hT, cT)) with [num_layers][H][B] device buffers;
+        the final (h, c) of this call is written to (hT, cT) (nn.LSTM's (h_n, c_n), unit-major)."""
         x = _as_input(x)
         B, H, T = x.shape
         _, (pwih, pbias, pwhh) = self.lstm.prepared(x.device)
@@ -275,8 +277,15 @@ class ResLSTM(nn.Module):
         ws = torch.empty(int(lib.bc_lstm_workspace_floats(B, H, T)), device=x.device, dtype=torch.float32)
         y = torch.empty_like(x)
         sa, sb = out_snake if out_snake is not None else (None, None)
-        L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
-               L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.stream_of(x))
+        if state is None:
+            L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
+                   L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.stream_of(x))
+            return y
+        init, (hT, cT) = state
+        h0, c0 = init if init is not None else (None, None)
+        L.call("bc_reslstm_fwd_state", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias,
+               pwhh, L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.ptr(h0), L.ptr(c0), hT.data_ptr(),
+               cT.data_ptr(), L.stream_of(x))
         return y
 
     def flow(self, x_raw, want_raw=True, next_act=None) -> Flow:

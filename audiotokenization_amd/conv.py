@@ -113,19 +113,24 @@ class Conv1dWN(_WNParams, nn.Module):
     def pad_left(self) -> int:
         return self.causal_pad if self.causal_pad is not None else self.padding
 
-    def out_len(self, T: int) -> int:
+    def out_len(self, T: int, pad_left: Optional[int] = None) -> int:
+        if pad_left is not None:  # explicit left pad, none on the right (streaming with carried context)
+            return (T + pad_left - self.dilation * (self.kernel_size - 1) - 1) // self.stride + 1
         pr = 0 if self.causal_pad is not None else self.padding
         return (T + self.pad_left() + pr - self.dilation * (self.kernel_size - 1) - 1) // self.stride + 1
 
-    def run(self, x, residual=None, epilogue: int = 0, out_snake=None, dual: bool = False):
+    def run(self, x, residual=None, epilogue: int = 0, out_snake=None, dual: bool = False,
+            pad_left: Optional[int] = None):
         """y = conv(x) + bias [+ residual]; then tanh (epilogue=1) or the next Snake (out_snake =
-        (alpha_exp, inv_beta)).  Returns y, or (raw, snake(raw)) when dual."""
+        (alpha_exp, inv_beta)).  Returns y, or (raw, snake(raw)) when dual.  pad_left overrides the
+        module's padding (left only; streaming.py passes 0 with the carried context prepended)."""
         x = _as_input(x)
         B, Cin, T = x.shape
         if Cin != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
         wp, bias, cfg = self.prepared(x.device)
-        Tout = self.out_len(T)
+        pl = self.pad_left() if pad_left is None else pad_left
+        Tout = self.out_len(T, pad_left)
         if Tout <= 0:
             raise ValueError(f"input length {T} too short for this convolution")
         y = torch.empty((B, self.out_channels, Tout), device=x.device, dtype=torch.float32)
@@ -139,7 +144,7 @@ class Conv1dWN(_WNParams, nn.Module):
         ev = tm.begin() if tm is not None else None
         L.call("bc_conv1d_fwd", x.data_ptr(), wp.data_ptr(), L.ptr(bias), L.ptr(residual), L.ptr(sa), L.ptr(sb),
                y.data_ptr(), L.ptr(y2), B, Cin, T, self.out_channels, Tout, self.kernel_size, self.stride,
-               self.dilation, self.pad_left(), epilogue, cfg, L.stream_of(x))
+               self.dilation, pl, epilogue, cfg, L.stream_of(x))
         if tm is not None:
             flops = 2.0 * B * self.out_channels * Cin * self.kernel_size * Tout
             nbytes = 4.0 * (x.numel() + y.numel() * (1 + (residual is not None) + dual))

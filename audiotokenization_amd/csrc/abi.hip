@@ -179,13 +179,39 @@ long long bc_lstm_workspace_floats(int B, int H, int T) {
   return tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq);
 }
 
+static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num_layers,
+                        const float* const* w_ih_packed, const float* const* bias,
+                        const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                        const float* out_snake_inv_beta, float* workspace, int mode, void* stream,
+                        const float* h0, const float* c0, float* hT, float* cT);
+
 int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_layers,
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
                    const float* out_snake_inv_beta, float* workspace, int mode, void* stream) {
+  return reslstm_impl(x, out, B, H, T, num_layers, w_ih_packed, bias, w_hh_packed, out_snake_alpha_exp,
+                      out_snake_inv_beta, workspace, mode, stream, nullptr, nullptr, nullptr, nullptr);
+}
+
+int bc_reslstm_fwd_state(const float* x, float* out, int B, int H, int T, int num_layers,
+                         const float* const* w_ih_packed, const float* const* bias,
+                         const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                         const float* out_snake_inv_beta, float* workspace, int mode, const float* h0,
+                         const float* c0, float* hT, float* cT, void* stream) {
+  if ((h0 == nullptr) != (c0 == nullptr) || (hT == nullptr) != (cT == nullptr)) return BC_ERR_ARG;
+  return reslstm_impl(x, out, B, H, T, num_layers, w_ih_packed, bias, w_hh_packed, out_snake_alpha_exp,
+                      out_snake_inv_beta, workspace, mode, stream, h0, c0, hT, cT);
+}
+
+static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num_layers,
+                        const float* const* w_ih_packed, const float* const* bias,
+                        const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                        const float* out_snake_inv_beta, float* workspace, int mode, void* stream,
+                        const float* h0, const float* c0, float* hT, float* cT) {
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
       H % 16 || T < 0 || num_layers <= 0 || mode < 0 || mode > 3)
     return BC_ERR_ARG;
+  const bool state = h0 || c0 || hT || cT;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   mode = lstm_mode(mode);
@@ -217,13 +243,16 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
     if (rc) return rc;
     if (lstm_use_seq(H, mode)) {
       // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
+      const long long so = (long long)l * H * B;  // layer l's [H][B] state
       rc = lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(w_hh_packed[l]), lout, cst, H, T, B,
-                           mode == 3 ? 2 : 3, st);
+                           mode == 3 ? 2 : 3, st, h0 ? h0 + so : nullptr, c0 ? c0 + so : nullptr,
+                           hT ? hT + so : nullptr, cT ? cT + so : nullptr);
       if (rc) return rc;
       lin = lout;
       lout = (lout == ya) ? yb : ya;
       continue;
     }
+    if (state) return BC_ERR_UNSUPPORTED;  // carried state: the persistent kernel only
     for (int t = 0; t < T; ++t) {
       rc = fast ? lstm_step_frag_launch(gx, w_hh_packed[l], frag[(t + 1) & 1], frag[t & 1], lout, cst,
                                         H, B, T, t, st)

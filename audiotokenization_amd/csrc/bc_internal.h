@@ -67,7 +67,8 @@ long long lstm_seq_packed_bytes(int H, int planes);
 void lstm_seq_pack(const float* w, unsigned short* out, int H, int planes);
 long long lstm_seq_workspace_bytes(int H, int T);
 int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
-                    int planes, hipStream_t st);
+                    int planes, hipStream_t st, const float* h0 = nullptr, const float* c0 = nullptr,
+                    float* hT = nullptr, float* cT = nullptr);
 int lstm_seq_read_status(int reset);
 int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
                      int T, int t, hipStream_t st);

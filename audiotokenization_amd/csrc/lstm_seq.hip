@@ -63,6 +63,13 @@ struct LstmSeqArgs {
   int H, T, Btot, b0, nb;
   int dbg;  // timing experiments only (BC_LSTM_SEQ_DEBUG): 4 = skip the flag poll (wrong results)
   long long* stamps;  // diagnostic s_memtime stamps (BC_LSTM_SEQ_STAMPS), nullptr in normal runs
+  // carried state (lstm_seq2 only; streaming): h0 / c0 [H][Btot] initial state or nullptr (zeros);
+  // hT / cT [H][Btot] final state or nullptr.  With h0, hseq slot 0 holds h0 and step t's h_t is
+  // published to slot t + 1 (flag t + 2).
+  const float* h0;
+  const float* c0;
+  float* hT;
+  float* cT;
 };
 
 constexpr int LS_STAMP_T = 2048;  // steps recorded per stamped workgroup
@@ -355,9 +362,60 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
   }
   const int cbh = (w & 1) * 16 + (lane & 15);  // my cell's clip within a half
   float cst0 = 0.f, cst1 = 0.f;                // my cell's c in half 0 / half 1
+  const long long unit_row = (long long)(g * LS_U + cu) * a.Btot + a.b0;  // [H][Btot] state row of my cell
+  if (a.c0) {
+    if (cbh < a.nb) cst0 = a.c0[unit_row + cbh];
+    if (NH + cbh < a.nb) cst1 = a.c0[unit_row + NH + cbh];
+  }
 
   const long long hhalf = (long long)H * (LS_NB * P / 2 / 2);  // floats of hseq per half-step
   const int nprod = G / LS_WAVES;
+  const int sh = a.h0 ? 1 : 0;  // hseq slot shift: slot 0 = h0
+
+  // h_t (or h0) of one half: gathered per clip in hs, split and written by wave 0 to hseq slot `slot`
+  auto publish_slot = [&](int slot, int h) {
+    if (w == 0 && lane < NH) {
+      const int nt = lane >> 4, c16 = lane & 15;
+      const int ksa = g >> 2, qq = g & 3;
+      const __amdgpu_buffer_rsrc_t hr = ls_rsrc(a.hseq + ((long long)slot * 2 + h) * hhalf, (unsigned)(hhalf * 4));
+      const unsigned off = (unsigned)((ksa * 2 + nt) * P * 1024 + (qq * 16 + c16) * 16);
+      float hv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hv[i] = hs[lane][i];
+      ls_u32x4 pl[P];
+      if constexpr (P == 2) {
+        unsigned hh[4], mm[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) split2_h(hv[2 * i] * 16384.0f, hv[2 * i + 1] * 16384.0f, hh[i], mm[i]);
+        pl[0] = (ls_u32x4){hh[0], hh[1], hh[2], hh[3]};
+        pl[1] = (ls_u32x4){mm[0], mm[1], mm[2], mm[3]};
+      } else {
+        ls_bf16x8 pb[3];
+        ls_split8(hv, pb);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) pl[p] = __builtin_bit_cast(ls_u32x4, pb[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) __builtin_amdgcn_raw_buffer_store_b128(pl[p], hr, off + p * 1024, 0, LS_SC1);
+    }
+  };
+  if (a.h0) {  // publish h0 of both halves to slot 0, then flags 1 (consumers of step 0 poll for them)
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      const int clip = h * NH + cbh;
+      hs[cbh][cu] = clip < a.nb ? a.h0[unit_row + clip] : 0.f;
+      __syncthreads();
+      publish_slot(0, h);
+      __syncthreads();
+    }
+    if (w == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        __hip_atomic_store(a.flags + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.flags + 256 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   ls_gu32* flags = (ls_gu32*)(a.flags);
   int pend_h = -1;        // wave 0: half whose h stores are issued but whose flag is not yet set
   unsigned pend_v = 0;
@@ -385,13 +443,13 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-      if (t > 0) {
+      if (t + sh > 0) {
         const ls_gu32* fl = flags + h * 256 + w * nprod;
         unsigned spins = 0;
         while (!(a.dbg & 4)) {
           const unsigned f = lane < nprod ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                           : 0xffffffffu;
-          if (__all(f >= (unsigned)t)) break;
+          if (__all(f >= (unsigned)(t + sh))) break;
           if (++spins > LS_SPIN_LIMIT) {
             if (lane == 0) {
               atomicAdd(a.status, 1);
@@ -404,7 +462,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         LS2_STAMP(1)
         const frag_t* hp =
-            reinterpret_cast<const frag_t*>(a.hseq + ((long long)(t - 1) * 2 + h) * hhalf) + lane;
+            reinterpret_cast<const frag_t*>(a.hseq + ((long long)(t - 1 + sh) * 2 + h) * hhalf) + lane;
         // h_{t-1} fragments through a register ring LS_HD k-steps deep: the loads of k-step ks + LS_HD - 1
         // are issued before k-step ks's MFMAs, so L2 latency hides behind LS_HD - 1 k-steps of MFMAs
         // (depth 2 left ~2300 of a half-step's 4600 load+MFMA cycles exposed, profiles/r01g_lstm_h3_stamps.txt)
@@ -474,7 +532,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
       float gt[4];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate)
-        gt[gate] = t > 0 ? gxv[gate] + (P == 2 ? hsum[gate] * gsc[gate] : hsum[gate]) : gxv[gate];
+        gt[gate] = t + sh > 0 ? gxv[gate] + (P == 2 ? hsum[gate] * gsc[gate] : hsum[gate]) : gxv[gate];
       const float ig = ls_sigmoid(gt[0]);
       const float fg = ls_sigmoid(gt[1]);
       const float gg = ls_tanh(gt[2]);
@@ -488,38 +546,17 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
       __syncthreads();
       LS2_STAMP(5)
 
-      if (w == 0 && t + 1 < a.T && lane < NH) {
-        const int nt = lane >> 4, c16 = lane & 15;
-        const int ksa = g >> 2, qq = g & 3;
-        const __amdgpu_buffer_rsrc_t hr =
-            ls_rsrc(a.hseq + ((long long)t * 2 + h) * hhalf, (unsigned)(hhalf * 4));
-        const unsigned off = (unsigned)((ksa * 2 + nt) * P * 1024 + (qq * 16 + c16) * 16);
-        float hv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) hv[i] = hs[lane][i];
-        ls_u32x4 pl[P];
-        if constexpr (P == 2) {
-          unsigned hh[4], mm[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) split2_h(hv[2 * i] * 16384.0f, hv[2 * i + 1] * 16384.0f, hh[i], mm[i]);
-          pl[0] = (ls_u32x4){hh[0], hh[1], hh[2], hh[3]};
-          pl[1] = (ls_u32x4){mm[0], mm[1], mm[2], mm[3]};
-        } else {
-          ls_bf16x8 pb[3];
-          ls_split8(hv, pb);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) pl[p] = __builtin_bit_cast(ls_u32x4, pb[p]);
-        }
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-          __builtin_amdgcn_raw_buffer_store_b128(pl[p], hr, off + p * 1024, 0, LS_SC1);
-      }
+      if (t + 1 < a.T) publish_slot(t + sh, h);
       if (w == 0 && t + 1 < a.T) {
         pend_h = h;
-        pend_v = (unsigned)(t + 1);
+        pend_v = (unsigned)(t + 1 + sh);
       }
       LS2_STAMP(6)
       if (ok) a.y[(long long)(g * LS_U + cu) * TB + (long long)t * a.Btot + a.b0 + clip] = hq;
+      if (t + 1 == a.T && ok) {  // carried state out
+        if (a.hT) a.hT[unit_row + clip] = hq;
+        if (a.cT) a.cT[unit_row + clip] = c;
+      }
 #undef LS2_STAMP
     }
   }
@@ -607,7 +644,7 @@ void lstm_seq_pack(const float* w, unsigned short* out, int H, int planes) {
 }
 
 long long lstm_seq_workspace_bytes(int H, int T) {
-  return LS_FLAG_BYTES + (long long)T * H * LS_HSTEP_PER_UNIT * 4;  // flags [2][256] | hseq
+  return LS_FLAG_BYTES + (long long)(T + 1) * H * LS_HSTEP_PER_UNIT * 4;  // flags [2][256] | hseq (+ h0 slot)
 }
 
 __device__ int bc_lstm_seq_timeouts;  // bumped by a workgroup that gave up waiting (never in a good run)
@@ -653,7 +690,7 @@ static int device_cus() {
 }
 
 int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
-                    int planes, hipStream_t st) {
+                    int planes, hipStream_t st, const float* h0, const float* c0, float* hT, float* cT) {
   if (planes != 2 && planes != 3) return BC_ERR_ARG;
   if (!lstm_seq_ok(H)) return BC_ERR_UNSUPPORTED;
   const int G = H / LS_U;
@@ -676,11 +713,16 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
   }();
   a.dbg = dbg;
   a.stamps = lstm_seq_stamp_buffer();
+  a.h0 = h0;
+  a.c0 = c0;
+  a.hT = hT;
+  a.cT = cT;
   // BC_LSTM_SEQ_HALVES=1: the single-batch kernel (kept for A/B timing), else two interleaved halves
   static const bool halves = [] {
     const char* e = getenv("BC_LSTM_SEQ_HALVES");
     return !(e && atoi(e) == 1);
   }();
+  if (!halves && (h0 || c0 || hT || cT)) return BC_ERR_UNSUPPORTED;  // carried state: lstm_seq2 only
   for (int b0 = 0; b0 < Btot; b0 += LS_NB) {
     a.b0 = b0;
     a.nb = Btot - b0 < LS_NB ? Btot - b0 : LS_NB;

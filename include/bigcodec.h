@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 5
+#define BC_ABI_VERSION 6
 
 int bc_abi_version(void);
 
@@ -128,6 +128,15 @@ int bc_reslstm_fwd(const float* x, float* out, int B, int H, int T, int num_laye
                    const float* const* w_ih_packed, const float* const* bias,
                    const float* const* w_hh_packed, const float* out_snake_alpha_exp,
                    const float* out_snake_inv_beta, float* workspace, int mode, void* stream);
+/* bc_reslstm_fwd_state: bc_reslstm_fwd with carried state for streaming (nn.LSTM's (h0, c0) in, (h_n, c_n)
+ *   out): h0 / c0 / hT / cT are [num_layers][H][B] device buffers (unit-major; NULL h0 and c0 = zero
+ *   state, NULL hT and cT = not returned).  Runs on the persistent kernel only (modes 1 and 3, H a
+ *   multiple of 128 up to 1536); other shapes return 3. */
+int bc_reslstm_fwd_state(const float* x, float* out, int B, int H, int T, int num_layers,
+                         const float* const* w_ih_packed, const float* const* bias,
+                         const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                         const float* out_snake_inv_beta, float* workspace, int mode, const float* h0,
+                         const float* c0, float* hT, float* cT, void* stream);
 
 /* ---- Factorized VQ (codebook_dim == 8) ---------------------------------------------------------
  * bc_vq_prepare_codebook: F.normalize(codebook) and its row sums of squares

@@ -1,0 +1,65 @@
+"""Causal streaming encode (audiotokenization_amd/streaming.py) on the MI355X.
+
+Property (size-independent, the reference has no streaming mode of its own): for a causal encoder the
+concatenated latents of a chunked stream equal the whole-sequence encode of the concatenated audio.
+  x6 precision (exact operand splits, tile-independent): two different chunkings agree BIT FOR BIT, and
+    with the whole-sequence pass (which runs the one-launch ResidualUnit) to max|d| / max|ref| <= 1e-6;
+  h3 precision (per-tile block scales): <= 1e-5;
+  VQ indices of stream and whole pass equal except certified near-ties (test_gpu_model.py's rule);
+and the whole-sequence causal encoder itself is checked against the CPU oracle on the same audio.
+"""
+import pytest
+import torch
+
+from audiotokenization_amd import _lib as L
+from audiotokenization_amd import synth
+from audiotokenization_amd.streaming import StreamingEncoder
+from helpers import assert_close_rel, build_models, index_mismatches, max_rel_err, top2_gap, torch_sd
+from oracle import bigcodec_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("model,B,chunks", [("base", 2, (1000, 3000)), ("debug", 2, (960, 1920)),
+                                            ("default", 1, (1200, 2400))])
+@pytest.mark.parametrize("sprec", ["x6", "h3"])
+def test_stream_equals_whole_sequence(dev, model, B, chunks, sprec):
+    old = L.precision_mode()
+    try:
+        L.set_precision(sprec)
+        enc, dec, esd, dsd, ek, _ = build_models(model, device=dev, causal=True)
+        n = 6000 if model != "debug" else 5760
+        x = torch.from_numpy(synth.synth_clips(B, n, clip0=11)).unsqueeze(1).to(dev)
+        s = StreamingEncoder(enc)
+        with torch.no_grad():
+            full = enc(x)
+            a = s.encode(x, chunks[0])
+            b = s.encode(x, chunks[1])
+            torch.cuda.synchronize()
+        assert a.shape == full.shape == b.shape
+        if sprec == "x6":
+            assert torch.equal(a, b), f"two chunkings differ: {max_rel_err(a, b):.3e}"
+        err = max_rel_err(a, full)
+        print(f"stream {model} [{sprec}] chunks {chunks}: max rel diff to the whole pass {err:.2e}, "
+              f"chunkings {max_rel_err(a, b):.2e}")
+        assert err <= (1e-6 if sprec == "x6" else 1e-5), err
+        with torch.no_grad():
+            c_full = dec(full, vq=True)[1].cpu()
+            c_a = dec(a, vq=True)[1].cpu()
+            lat_ref = O.encoder_forward(x.cpu(), torch_sd(esd), ek)
+            _, _, _, ze = O.fvq_forward(lat_ref, torch_sd(dsd), "quantizer.layers.0.", return_ze=True)
+        gap = top2_gap(ze, torch.from_numpy(dsd["quantizer.layers.0._codebook.weight"]))
+        index_mismatches(c_a.numpy(), c_full.numpy(), gap)
+        assert_close_rel(full.cpu(), lat_ref, 1e-4, "causal whole-sequence latent vs oracle")
+    finally:
+        L._mode = old
+
+
+def test_stream_rejects_bad_chunks_and_non_causal(dev):
+    enc, *_ = build_models("debug", device=dev, causal=True)
+    s = StreamingEncoder(enc)
+    with pytest.raises(ValueError):
+        s.push(torch.zeros(1, 1, 321, device=dev))
+    enc_nc, *_ = build_models("debug", device=dev)
+    with pytest.raises(ValueError):
+        StreamingEncoder(enc_nc)
