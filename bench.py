@@ -70,6 +70,24 @@ def kernel_peak(kname: str):
     return FP32_MFMA_PEAK_TFLOPS, 1, "native fp32 MFMA peak"
 
 
+def kernel_table(summ, steps, probe, n=8):
+    """The n most time-consuming HIP-event-timed kernels of the timed steps: ms per step, algorithmic
+    TFLOP/s against the kernel's MFMA ceiling (spec and probe-measured) and algorithmic GB/s against
+    the 8 TB/s HBM peak.  The kernels' rows are the ones bench's roofline entry is drawn from."""
+    rows = []
+    for name, d in sorted(summ.items(), key=lambda kv: -kv[1]["ms_total"])[:n]:
+        sec = d["ms_total"] * 1e-3
+        tf = d["flops_total"] / sec / 1e12
+        peak, mult, _ = kernel_peak(name)
+        gbs = d["bytes_total"] / sec / 1e9
+        rows.append({"kernel": name, "launches_per_step": d["launches"] // steps,
+                     "ms_per_step": round(d["ms_total"] / steps, 3), "tflops": round(tf, 1),
+                     "frac_mfma_spec": round(tf / peak, 3),
+                     "frac_mfma_probe": round(tf * mult / probe, 3) if name.startswith(("conv1d_x6", "resunit_x6")) else None,
+                     "gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 3)})
+    return rows
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -309,7 +327,8 @@ def main():
                 "launches_per_step": d["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_gflop_per_launch": round(d["flops_total"] / d["launches"] / 1e9, 3),
                 "all_python_conv_kernels_ms_per_step": round(conv_ms / args.steps, 2),
-                "all_python_conv_tflops": round(sum(v["flops_total"] for v in summ.values()) / (conv_ms * 1e-3) / 1e12, 2)}
+                "all_python_conv_tflops": round(sum(v["flops_total"] for v in summ.values()) / (conv_ms * 1e-3) / 1e12, 2),
+                "kernels_top": kernel_table(summ, args.steps, probe)}
 
     cpu = None
     parity = None
