@@ -28,6 +28,7 @@ _SIGS = {
     "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
     "bc_resunit_select_cfg": (I, [I, I, I]),
     "bc_resunit_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "bc_resunit_fwd_snake_in": (I, [P] * 13 + [I] * 6 + [P]),
     "bc_convT1d_phase_taps": (I, [I, I]),
     "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
@@ -52,7 +53,7 @@ _SIGS = {
     "bc_synth_clips": (I, [P, I, L, L, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 6  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 7  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

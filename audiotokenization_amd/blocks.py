@@ -13,6 +13,7 @@ an epilogue; they run as their own kernel on the raw output.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -91,36 +92,55 @@ class ResidualUnit(nn.Module):
         conv7 = _conv_of(self.block[1])
         return L.load().bc_resunit_select_cfg(conv7.in_channels, conv7.dilation, mode)
 
+    def snake_on_load(self) -> bool:
+        """True when the one-launch kernel applies the first Snake while staging its input
+        (bc_resunit_fwd_snake_in): the producer then writes the raw tensor only (x_act=None).
+        BIGCODEC_RU_SNAKE_IN=0 restores producer-side activation (dual raw + activated outputs)."""
+        if not _fusable(self.first_act) or os.environ.get("BIGCODEC_RU_SNAKE_IN", "1") == "0":
+            return False
+        return self._fused_cfg() >= 0
+
     def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
-        """x_act = self.first_act(x_raw) (computed by the producer)."""
+        """x_act = self.first_act(x_raw) computed by the producer, or None (snake_on_load)."""
         if next_act is None or _fusable(next_act):
             cfg = self._fused_cfg()
             if cfg >= 0:
                 return self._flow_fused(cfg, x_raw, x_act, want_raw, next_act)
+        if x_act is None:
+            x_act = self.first_act(x_raw)
         _, h = produce_conv(self.block[1], x_act, None, want_raw=False, next_act=self.block[2])
         return produce_conv(self.block[3], h, residual=x_raw, want_raw=want_raw, next_act=next_act)
 
     def _flow_fused(self, cfg, x_raw, x_act, want_raw, next_act) -> Flow:
         conv7, conv1 = _conv_of(self.block[1]), _conv_of(self.block[3])
-        dev = x_act.device
+        lazy = x_act is None and _fusable(self.first_act)
+        if x_act is None and not lazy:
+            x_act = self.first_act(x_raw)
+        dev = x_raw.device
         w7, b7 = conv7.packed_as(cfg, dev)
         w1, b1 = conv1.packed_as(cfg, dev)
         s2a, s2b = self.block[2].act.coeffs(dev)
-        B, C, T = x_act.shape
-        if x_raw.shape != x_act.shape:
+        B, C, T = x_raw.shape
+        if not lazy and x_raw.shape != x_act.shape:
             raise ValueError("ResidualUnit: raw and activated inputs differ in shape")
         sa, sb = next_act.act.coeffs(dev) if next_act is not None else (None, None)
         dual = next_act is not None and want_raw
-        y = torch.empty_like(x_act)
-        y2 = torch.empty_like(x_act) if dual else None
+        y = torch.empty_like(x_raw)
+        y2 = torch.empty_like(x_raw) if dual else None
         tm = L.active_timer()
         ev = tm.begin() if tm is not None else None
-        L.call("bc_resunit_fwd", x_raw.data_ptr(), x_act.data_ptr(), w7.data_ptr(), L.ptr(b7), s2a.data_ptr(),
-               s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb), y.data_ptr(), L.ptr(y2),
-               B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_act))
+        if lazy:
+            s1a, s1b = self.first_act.act.coeffs(dev)
+            L.call("bc_resunit_fwd_snake_in", x_raw.data_ptr(), s1a.data_ptr(), s1b.data_ptr(), w7.data_ptr(),
+                   L.ptr(b7), s2a.data_ptr(), s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb),
+                   y.data_ptr(), L.ptr(y2), B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_raw))
+        else:
+            L.call("bc_resunit_fwd", x_raw.data_ptr(), x_act.data_ptr(), w7.data_ptr(), L.ptr(b7),
+                   s2a.data_ptr(), s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb), y.data_ptr(),
+                   L.ptr(y2), B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_raw))
         if tm is not None:
             flops = 2.0 * B * C * C * T * 8  # k=7 and k=1
-            nbytes = 4.0 * x_act.numel() * (3 + dual)
+            nbytes = 4.0 * x_raw.numel() * ((2 if lazy else 3) + dual)
             tm.end(ev, L.resunit_kernel_name(cfg, C, conv7.dilation), flops, nbytes)
         if next_act is None:
             return y, None
@@ -130,7 +150,16 @@ class ResidualUnit(nn.Module):
 
     def forward(self, x):
         x = _as_input(x)
-        return self.flow(x, self.first_act(x))[0]
+        return self.flow(x, None if self.snake_on_load() else self.first_act(x))[0]
+
+
+def input_act(stage) -> Optional[Activation1d]:
+    """The activation a producer must apply for `stage` (a ResidualUnit / Encoder- / DecoderBlock);
+    None when the stage's first ResidualUnit activates on load (raw output only)."""
+    first = stage if isinstance(stage, ResidualUnit) else stage.block[0]
+    if isinstance(first, ResidualUnit) and first.snake_on_load():
+        return None
+    return stage.first_act
 
 
 class EncoderBlock(nn.Module):
@@ -157,13 +186,13 @@ class EncoderBlock(nn.Module):
         rus = [self.block[i] for i in range(n - 2)]
         for i, ru in enumerate(rus):
             last = i == len(rus) - 1
-            nxt = self.block[n - 2] if last else rus[i + 1].first_act
+            nxt = self.block[n - 2] if last else input_act(rus[i + 1])
             x_raw, x_act = ru.flow(x_raw, x_act, want_raw=not last, next_act=nxt)
         return produce_conv(self.block[n - 1], x_act, None, want_raw=want_raw, next_act=next_act)
 
     def forward(self, x):
         x = _as_input(x)
-        return self.flow(x, self.first_act(x))[0]
+        return self.flow(x, None if input_act(self) is None else self.first_act(x))[0]
 
 
 class DecoderBlock(nn.Module):
@@ -192,11 +221,11 @@ class DecoderBlock(nn.Module):
     def flow(self, x_raw, x_act, want_raw=True, next_act=None) -> Flow:
         rus = [self.block[i] for i in range(2, len(self.block))]
         y_raw, y_act = produce_convT(self.block[1], x_act, want_raw=True,
-                                     next_act=rus[0].first_act if rus else next_act)
+                                     next_act=input_act(rus[0]) if rus else next_act)
         for i, ru in enumerate(rus):
             last = i == len(rus) - 1
             y_raw, y_act = ru.flow(y_raw, y_act, want_raw=(want_raw if last else True),
-                                   next_act=next_act if last else rus[i + 1].first_act)
+                                   next_act=next_act if last else input_act(rus[i + 1]))
         return y_raw, y_act
 
     def forward(self, x):

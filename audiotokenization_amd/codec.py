@@ -10,7 +10,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .blocks import DecoderBlock, EncoderBlock, ResLSTM, produce_conv
+from .blocks import DecoderBlock, EncoderBlock, ResLSTM, input_act, produce_conv
 from .conv import WNConv1d
 from .modules import FSQ, Activation1d, ResidualVQ, SnakeBeta, _as_input, _zeros
 
@@ -56,7 +56,7 @@ class BigCodecEncoder(nn.Module):
         def next_act_of(i):
             if i + 1 < len(stages):
                 nxt = stages[i + 1]
-                return nxt.first_act if isinstance(nxt, EncoderBlock) else None  # ResLSTM takes raw
+                return input_act(nxt) if isinstance(nxt, EncoderBlock) else None  # ResLSTM takes raw
             return final_act
         y, ya = produce_conv(blk[0], x, None, want_raw=True, next_act=next_act_of(-1) if stages else final_act)
         for i, st in enumerate(stages):

@@ -84,6 +84,24 @@ int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packe
                         S(stream));
 }
 
+int bc_resunit_fwd_snake_in(const float* x_raw, const float* in_snake_alpha_exp, const float* in_snake_inv_beta,
+                            const float* w7_packed, const float* b7, const float* mid_snake_alpha_exp,
+                            const float* mid_snake_inv_beta, const float* w1_packed, const float* b1,
+                            const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y, float* y2,
+                            int B, int C, int T, int dilation, int pad_left, int cfg, void* stream) {
+  if (!x_raw || !in_snake_alpha_exp || !in_snake_inv_beta || !w7_packed || !w1_packed || !mid_snake_alpha_exp ||
+      !mid_snake_inv_beta || !y || B < 0 || C <= 0 || T < 0 || dilation <= 0 || pad_left < 0 ||
+      pad_left > 6 * dilation)
+    return BC_ERR_ARG;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
+  if (cfg != resunit_select_cfg(C, dilation, 1) && cfg != resunit_select_cfg(C, dilation, 3)) return BC_ERR_ARG;
+  if (B == 0 || T == 0) return BC_OK;
+  return resunit_launch(x_raw, x_raw, w7_packed, b7, mid_snake_alpha_exp, mid_snake_inv_beta, w1_packed, b1,
+                        out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, C, T, dilation, pad_left, cfg,
+                        S(stream), in_snake_alpha_exp, in_snake_inv_beta);
+}
+
 int bc_convT1d_phase_taps(int K, int stride) {
   if (K <= 0 || stride <= 0) return -1;
   return (K + stride - 1) / stride;

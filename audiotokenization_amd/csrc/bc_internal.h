@@ -46,7 +46,8 @@ int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
 int resunit_select_cfg(int C, int d, int mode);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
-                   float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st);
+                   float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
+                   const float* isa = nullptr, const float* isb = nullptr);
 
 int snake_launch(const float* x, const float* sa, const float* sb, float* y, int B, int C,
                  long long T, hipStream_t st);

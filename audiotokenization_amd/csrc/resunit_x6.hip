@@ -36,6 +36,10 @@ struct RUExtra {
   int hplane;        // bytes per Hs plane = nck1 * BN * 64
   int nck1;          // 32-channel chunks of the k=1 conv's input
   int dbg;           // BC_RU_DEBUG timing experiments (wrong results): 1 no A copies, 2 no B loads, 4 no epilogue, 8 no phase 2
+  // snake on load: the unit's first Activation1d applied while staging the k=7 input (x_act == x_raw,
+  // isa / isb = its alpha_exp / inv_beta), so the producer writes only the raw tensor; nullptr: x_act given
+  const float* isa;
+  const float* isb;
 };
 
 __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
@@ -133,6 +137,19 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
     return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
   };
   float xs = 1.f;  // P == 2: scale of the staged k=7 input chunk and of the phase-1 accumulator
+  // snake on load (r.isa): activate the thread's two staged channels of `chunk` in registers (out-of-range
+  // loads read 0 and snake(0) = 0: the zero padding of the activated signal, as the reference pads it)
+  auto activate_b = [&](int chunk) {
+    if (!r.isa) return;
+    const int ci0 = chunk * X6_BKC + 2 * bp;
+    const float a0 = ci0 < a.Cin ? r.isa[ci0] : 0.f, b0 = ci0 < a.Cin ? r.isb[ci0] : 0.f;
+    const float a1 = ci0 + 1 < a.Cin ? r.isa[ci0 + 1] : 0.f, b1 = ci0 + 1 < a.Cin ? r.isb[ci0 + 1] : 0.f;
+#pragma unroll
+    for (int i = 0; i < CI; ++i) {
+      bv0[i] = snake(bv0[i], a0, b0);
+      bv1[i] = snake(bv1[i], a1, b1);
+    }
+  };
   auto store_b = [&]() {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
@@ -180,6 +197,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 
   issue_a(a.w, 0, 0);
   load_b(0);
+  activate_b(0);
   if constexpr (P == 2) {
     bmax_publish(0);
     lds_barrier();
@@ -244,6 +262,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       }
       }
       if (tp == kst - 1 && c + 1 < a.nchunks) {
+        activate_b(c + 1);
         if constexpr (P == 2) bmax_publish((c + 1) & 1);
         lds_barrier();
         if constexpr (P == 2) h3_next_scale((c + 1) & 1);
@@ -499,7 +518,8 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
-                   float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st) {
+                   float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
+                   const float* isa, const float* isb) {
   ConvArgs a{};
   a.x = x_act; a.w = w7; a.bias = b7;
   a.xbs = (long long)C * T;
@@ -514,7 +534,8 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
     const char* v = getenv("BC_RU_DEBUG");
     return v ? atoi(v) : 0;
   }();
-  RUExtra r{w1, s2a, s2b, 0, 0, dbg};
+  RUExtra r{w1, s2a, s2b, 0, 0, dbg, isa, isb};
+  if (isa) a.x = x_raw;  // snake on load
 #define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
   case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \
   case 300 + ID: return launch_ru<MT, NT, WM, WN, 2>(a, e, r, B, st);

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 6
+#define BC_ABI_VERSION 7
 
 int bc_abi_version(void);
 
@@ -71,6 +71,13 @@ int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packe
                    const float* w1_packed, const float* b1, const float* out_snake_alpha_exp,
                    const float* out_snake_inv_beta, float* y, float* y2, int B, int C, int T,
                    int dilation, int pad_left, int cfg, void* stream);
+/* bc_resunit_fwd_snake_in: the same unit with its FIRST Activation1d applied while the k=7 input is
+ *   staged (x_act = snake_in(x_raw) is never materialised: the producer writes only x_raw). */
+int bc_resunit_fwd_snake_in(const float* x_raw, const float* in_snake_alpha_exp, const float* in_snake_inv_beta,
+                            const float* w7_packed, const float* b7, const float* mid_snake_alpha_exp,
+                            const float* mid_snake_inv_beta, const float* w1_packed, const float* b1,
+                            const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y, float* y2,
+                            int B, int C, int T, int dilation, int pad_left, int cfg, void* stream);
 
 /* ---- ConvTranspose1d (weight-normed, fused next-Snake epilogue) -------------------------------
  * Replaces: weight_norm(nn.ConvTranspose1d) (vq/module.py:67-72) and CausalConvTranspose1d

@@ -275,12 +275,19 @@ def test_resunit_fused(dev, C, d, causal, B, T, ru_prec):
         got = ru.flow(xd, xa)[0].cpu()
         raw, act = ru.flow(xd, xa, want_raw=True, next_act=nxt)
         _, act_only = ru.flow(xd, xa, want_raw=False, next_act=nxt)
+        # snake on load (bc_resunit_fwd_snake_in): the first Snake applied while staging the raw input
+        # computes the same operations in the same order as the producer epilogue -> bit-identical
+        assert ru.snake_on_load()
+        lazy = ru.flow(xd, None)[0].cpu()
+        lraw, lact = ru.flow(xd, None, want_raw=True, next_act=nxt)
     finally:
         L._mode = old
     assert_close_rel(got, want, 2e-5, f"resunit C={C} d={d}")
     assert torch.equal(raw.cpu(), got)
     assert_close_rel(act.cpu(), want_s, 5e-5, "resunit + next snake")
     assert torch.equal(act_only.cpu(), act.cpu())
+    assert torch.equal(lazy, got)
+    assert torch.equal(lraw.cpu(), got) and torch.equal(lact.cpu(), act.cpu())
 
 
 @pytest.mark.parametrize("Cin,Cout,K,s,d", [(384, 384, 7, 1, 9), (48, 96, 4, 2, 1), (768, 768, 1, 1, 1)])
