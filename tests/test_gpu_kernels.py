@@ -391,6 +391,54 @@ def test_fvq_forward_and_vq2emb(dev):
     assert_close_rel(emb, want_emb, 1e-6, "vq2emb")
 
 
+@pytest.mark.parametrize("nq", [2, 4])
+def test_multi_quantizer_rvq(dev, nq):
+    """vq_num_quantizers > 1 (residual_vq.py:21-40): each layer quantizes the
+    residual the previous ones left.  Indices (nq, B, F) against the oracle: a frame may differ only
+    after a certified fp32 near-tie (first differing layer's oracle top-2 gap < 1e-5; later layers then
+    see another residual), at most 2 frames; z_q within 1e-5 on the frames that agree; loss (nq,) zeros;
+    vq2emb on the oracle's codes within 1e-6."""
+    g = torch.Generator().manual_seed(23 + nq)
+    D = 96
+    rvq = M.ResidualVQ(num_quantizers=nq, dim=D, codebook_size=8192, codebook_dim=8, commitment=0.25)
+    with torch.no_grad():
+        for p in rvq.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.3)
+    rvq.eval()
+    z = torch.randn(2, D, 333, generator=g)
+    sd = {k: v.detach() for k, v in rvq.state_dict().items()}
+    want_q, want_idx, _ = O.rvq_forward(z, sd, "", nq)
+    rvq.to(dev)
+    got_q, got_idx, loss = rvq(z.to(dev))
+    torch.cuda.synchronize()
+    assert tuple(got_idx.shape) == (nq, 2, 333) and tuple(loss.shape) == (nq,)
+    assert float(loss.abs().sum()) == 0.0
+    gi, wi = got_idx.cpu().numpy().reshape(nq, -1), want_idx.numpy().reshape(nq, -1)
+    bad = np.nonzero((gi != wi).any(0))[0]
+    # certify each differing frame at its first differing layer, on the oracle's own residual there
+    res = z.clone()
+    gaps = {}
+    for q in range(nq):
+        pre = f"layers.{q}."
+        zq, _, _, ze = O.fvq_forward(res, sd, pre, return_ze=True)
+        _, best, second = vq_c.argmin(ze.permute(0, 2, 1).reshape(-1, 8).numpy(),
+                                      sd[pre + "_codebook.weight"].numpy(), return_dists=True)
+        for f in bad:
+            if f not in gaps and gi[q, f] != wi[q, f]:
+                gaps[f] = float(second[f] - best[f])
+        res = res - zq
+    print(f"nq={nq}: {bad.size} differing frames of {gi.shape[1]}, gaps {sorted(gaps.values())}")
+    assert bad.size <= 2 and all(v < 1e-5 for v in gaps.values())
+    ok = np.ones(gi.shape[1], bool)
+    ok[bad] = False
+    gq = got_q.cpu().permute(0, 2, 1).reshape(-1, D)[ok]
+    wq = want_q.permute(0, 2, 1).reshape(-1, D)[ok]
+    assert_close_rel(gq, wq, 1e-5, f"rvq nq={nq} post")
+    vq = want_idx.permute(1, 2, 0).contiguous()
+    emb = rvq.vq2emb(vq.to(dev)).cpu()
+    assert_close_rel(emb, O.vq2emb(vq, sd, "", nq), 1e-6, f"rvq nq={nq} vq2emb")
+
+
 def test_synth_clips_device_equals_host(dev):
     from audiotokenization_amd import synth
     from audiotokenization_amd.extract import synth_batch
