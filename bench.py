@@ -188,11 +188,22 @@ def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
                 zq, _, _ = O.rvq_forward(emb, sds[1], "quantizer.", dk.get("vq_num_quantizers", 1))
                 wavs.append(O.decoder_forward(zq, sds[1], dk))
         dt = time.perf_counter() - t0
+        # also the batched CPU rate (the same clips as one B = n_clips call); best of both
+        dtb = None
+        if not roundtrip and n_clips > 1:
+            t0 = time.perf_counter()
+            O.encode_indices(x, sds[0], sds[1], ek, dk)
+            dtb = time.perf_counter() - t0
     audio_s = n_clips * n_samples / 24000.0
     what = "encode+VQ+decode" if roundtrip else "encode+VQ"
-    return (dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port",
-                 sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz, {name} model, {what}, B=1 "
-                        f"(extract_indices.py:397), torch CPU oracle, {dt:.1f} s"),
+    rates = {"B=1": audio_s / dt}
+    if dtb:
+        rates[f"B={n_clips}"] = audio_s / dtb
+    best = max(rates, key=rates.get)
+    return (dict(value=rates[best], unit="audio-sec/s", cores=threads, kind="port", rates=rates,
+                 sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz, {name} model, {what}, best of "
+                        f"{'/'.join(rates)} ({best}; B=1 is extract_indices.py:397), torch CPU oracle, "
+                        f"{dt + (dtb or 0):.1f} s"),
             torch.cat(codes, dim=1), torch.cat(wavs, dim=0) if roundtrip else None)
 
 
