@@ -51,9 +51,10 @@ _SIGS = {
     "bc_btc_to_ctb": (I, [P, P, I, I, I, P]),
     "bc_ctb_to_btc_add": (I, [P, P, P, I, I, I, P]),
     "bc_synth_clips": (I, [P, I, L, L, P]),
+    "bc_tanh_fwd": (I, [P, P, L, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 7  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 8  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -100,6 +101,49 @@ def call(name: str, *args) -> int:
     rc = getattr(lib, name)(*args)
     check(rc, name)
     return rc
+
+
+_pending_status = []  # (device int32 status tensor, what) of launches not yet checked
+
+
+def defer_status(status, what: str) -> None:
+    """Remember a device status word (nonzero = the launch failed, e.g. a persistent-kernel timeout,
+    include/bigcodec.h) to be checked by check_status() before the caller's output is consumed."""
+    _pending_status.append((status, what))
+
+
+def check_status() -> None:
+    """Read every pending status word (ONE device -> host copy, which waits for the stream) and raise
+    BigCodecLibraryError if any launch reported a failure.  Called at the end of each codec forward
+    (encoder, decoder, streaming push, standalone ResLSTM)."""
+    global _pending_status
+    if not _pending_status:
+        return
+    import torch
+
+    items, _pending_status = _pending_status, []
+    vals = torch.cat([t.reshape(-1) for t, _ in items]).cpu().tolist()
+    bad = [f"{what}: {v} workgroup(s) timed out" for (_, what), v in zip(items, vals) if v]
+    if bad:
+        raise BigCodecLibraryError("persistent LSTM launch failed, its output is wrong (" + "; ".join(bad) +
+                                   "). The H/8 workgroups of the recurrence must be co-resident; another "
+                                   "kernel holding CUs for seconds can starve them.")
+
+
+def conv_cfg(Cout: int, Cin: int, K: int, stride: int, dilation: int, mode: int) -> int:
+    """bc_conv1d_select_cfg, checked: a negative answer (no tile for the shape) raises."""
+    cfg = load().bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode)
+    if cfg < 0:
+        raise BigCodecLibraryError(f"bc_conv1d_select_cfg: no conv tile for Cout={Cout} Cin={Cin} K={K} "
+                                   f"stride={stride} dilation={dilation} mode={mode} (returned {cfg})")
+    return cfg
+
+
+def checked_size(n: int, what: str) -> int:
+    """A size query's answer (bc_*_packed_floats / bc_lstm_workspace_floats), checked: negative raises."""
+    if n < 0:
+        raise BigCodecLibraryError(f"{what} returned {n}: the shape or tile is not supported")
+    return int(n)
 
 
 def ptr(t) -> int | None:

@@ -266,15 +266,17 @@ class LSTM(nn.Module):
             if self.input_size != H:
                 raise NotImplementedError("ResLSTM requires input_size == hidden_size")
             mode = L.lstm_mode()
-            cfg = lib.bc_conv1d_select_cfg(4 * H, H, 1, 1, 1, mode)
+            cfg = L.conv_cfg(4 * H, H, 1, 1, 1, mode)
             wih, whh, bias = [], [], []
             for l in range(self.num_layers):
                 w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
-                packed = np.empty(lib.bc_conv1d_packed_floats(4 * H, H, 1, cfg), dtype=np.float32)
+                packed = np.empty(L.checked_size(lib.bc_conv1d_packed_floats(4 * H, H, 1, cfg), "bc_conv1d_packed_floats"),
+                                  dtype=np.float32)
                 L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
                 wih.append(torch.from_numpy(packed).to(device))
                 w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
-                packed = np.empty(lib.bc_lstm_hh_packed_floats(H, mode), dtype=np.float32)
+                packed = np.empty(L.checked_size(lib.bc_lstm_hh_packed_floats(H, mode), "bc_lstm_hh_packed_floats"),
+                                  dtype=np.float32)
                 L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, mode)
                 whh.append(torch.from_numpy(packed).to(device))
                 b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
@@ -303,18 +305,22 @@ class ResLSTM(nn.Module):
         B, H, T = x.shape
         _, (pwih, pbias, pwhh) = self.lstm.prepared(x.device)
         lib = L.load()
-        ws = torch.empty(int(lib.bc_lstm_workspace_floats(B, H, T)), device=x.device, dtype=torch.float32)
+        ws = torch.empty(L.checked_size(lib.bc_lstm_workspace_floats(B, H, T), "bc_lstm_workspace_floats"),
+                         device=x.device, dtype=torch.float32)
         y = torch.empty_like(x)
         sa, sb = out_snake if out_snake is not None else (None, None)
         if state is None:
             L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
                    L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.stream_of(x))
-            return y
-        init, (hT, cT) = state
-        h0, c0 = init if init is not None else (None, None)
-        L.call("bc_reslstm_fwd_state", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias,
-               pwhh, L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.ptr(h0), L.ptr(c0), hT.data_ptr(),
-               cT.data_ptr(), L.stream_of(x))
+        else:
+            init, (hT, cT) = state
+            h0, c0 = init if init is not None else (None, None)
+            L.call("bc_reslstm_fwd_state", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias,
+                   pwhh, L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.ptr(h0), L.ptr(c0),
+                   hT.data_ptr(), cT.data_ptr(), L.stream_of(x))
+        # include/bigcodec.h: ((int*)workspace)[0] counts persistent workgroups that timed out; the
+        # codec's forward checks it (L.check_status) before its output can be consumed
+        L.defer_status(ws[:1].view(torch.int32).clone(), f"ResLSTM(H={H}, layers={self.lstm.num_layers}, T={T})")
         return y
 
     def flow(self, x_raw, want_raw=True, next_act=None) -> Flow:
@@ -326,4 +332,6 @@ class ResLSTM(nn.Module):
         return y, next_act(y)
 
     def forward(self, x):
-        return self.run(x)
+        y = self.run(x)
+        L.check_status()
+        return y

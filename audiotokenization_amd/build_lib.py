@@ -25,6 +25,8 @@ SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip"
 HEADERS = ["bc_common.h", "bc_internal.h", "conv_epilogue.h", "x6_common.h", "conv1d_x6_kernel.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
+if os.environ.get("BIGCODEC_ABLATION") == "1":  # tools/*_ablation.sh only: compiles the work-skipping switches in
+    CFLAGS.append("-DBC_ABLATION")
 
 
 def _hipcc() -> str:

@@ -10,16 +10,21 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import _lib as L
 from .blocks import DecoderBlock, EncoderBlock, ResLSTM, input_act, produce_conv
 from .conv import WNConv1d
 from .modules import FSQ, Activation1d, ResidualVQ, SnakeBeta, _as_input, _zeros
 
 
 class _Tanh(nn.Module):
-    """nn.Tanh position holder (codec_decoder.py:80); it runs fused in the last conv's epilogue."""
+    """nn.Tanh (codec_decoder.py:80).  decode() runs it fused in the last conv's epilogue; called on its
+    own (decoder.model used as the reference's nn.Sequential) it is bc_tanh_fwd."""
 
     def forward(self, x):
-        raise NotImplementedError("the decoder's final tanh runs fused in the last conv's epilogue")
+        x = _as_input(x)
+        y = torch.empty_like(x)
+        L.call("bc_tanh_fwd", x.data_ptr(), y.data_ptr(), x.numel(), L.stream_of(x))
+        return y
 
 
 class BigCodecEncoder(nn.Module):
@@ -66,7 +71,9 @@ class BigCodecEncoder(nn.Module):
                 y, ya = st.flow(y, ya, want_raw=want_raw, next_act=nact)
             else:
                 y, ya = st.flow(y, want_raw=want_raw, next_act=nact)
-        return produce_conv(last_conv, ya, None, want_raw=True, next_act=None)[0]
+        out = produce_conv(last_conv, ya, None, want_raw=True, next_act=None)[0]
+        L.check_status()  # a failed persistent ResLSTM launch raises here, before the latent is used
+        return out
 
     def inference(self, x):
         return self.forward(x)
@@ -137,7 +144,9 @@ class BigCodecDecoder(nn.Module):
                 y, ya = st.flow(y, ya, want_raw=want_raw, next_act=nact)
             else:
                 y, ya = st.flow(y, want_raw=want_raw, next_act=nact)
-        return produce_conv(last_conv, ya, None, want_raw=True, next_act=None, epilogue=1)[0]
+        out = produce_conv(last_conv, ya, None, want_raw=True, next_act=None, epilogue=1)[0]
+        L.check_status()
+        return out
 
     def forward(self, x, vq=True):
         if vq is True:

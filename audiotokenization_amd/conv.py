@@ -89,8 +89,9 @@ class Conv1dWN(_WNParams, nn.Module):
             w = self.folded_weight().contiguous()
             Cout, Cin, K = w.shape
             lib = L.load()
-            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, self.stride, self.dilation, L.precision_mode())
-            packed = np.empty(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg), dtype=np.float32)
+            cfg = L.conv_cfg(Cout, Cin, K, self.stride, self.dilation, L.precision_mode())
+            packed = np.empty(L.checked_size(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg),
+                                             f"bc_conv1d_packed_floats({Cout}, {Cin}, {K}, cfg {cfg})"), dtype=np.float32)
             L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, Cout, Cin, K, cfg)
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return torch.from_numpy(packed).to(device), bias, cfg
@@ -102,7 +103,8 @@ class Conv1dWN(_WNParams, nn.Module):
             w = self.folded_weight().contiguous()
             Cout, Cin, K = w.shape
             lib = L.load()
-            packed = np.empty(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg), dtype=np.float32)
+            packed = np.empty(L.checked_size(lib.bc_conv1d_packed_floats(Cout, Cin, K, cfg),
+                                             f"bc_conv1d_packed_floats({Cout}, {Cin}, {K}, cfg {cfg})"), dtype=np.float32)
             L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, Cout, Cin, K, cfg)
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return torch.from_numpy(packed).to(device), bias
@@ -213,8 +215,9 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
             s = self.stride
             lib = L.load()
             Kp = lib.bc_convT1d_phase_taps(K, s)
-            cfg = lib.bc_conv1d_select_cfg(Cout, Cin, Kp, 1, 1, L.precision_mode())
-            n = lib.bc_conv1d_packed_floats(Cout, Cin, Kp, cfg)
+            cfg = L.conv_cfg(Cout, Cin, Kp, 1, 1, L.precision_mode())
+            n = L.checked_size(lib.bc_conv1d_packed_floats(Cout, Cin, Kp, cfg),
+                               f"bc_conv1d_packed_floats({Cout}, {Cin}, {Kp}, cfg {cfg})")
             wt = w.permute(1, 0, 2).contiguous()  # (Cout, Cin, K)
             phases = []
             for r in range(s):

@@ -186,7 +186,9 @@ int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode)
   return BC_OK;
 }
 
-// workspace: xt [H][T*B] | gx [4H][T*B] | y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2
+// workspace: status [64 floats: int32 timeout count of this call] | xt [H][T*B] | gx [4H][T*B] |
+// y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2
+constexpr long long LSTM_WS_STATUS_FLOATS = 64;
 static long long lstm_frag_floats(int B, int H) { return (long long)((B + 63) / 64) * 64 * H; }
 
 long long bc_lstm_workspace_floats(int B, int H, int T) {
@@ -194,7 +196,7 @@ long long bc_lstm_workspace_floats(int B, int H, int T) {
   const long long tb = (long long)T * B;
   const long long frag = 2 * lstm_frag_floats(B, H);
   const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
-  return tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq);
+  return LSTM_WS_STATUS_FLOATS + tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq);
 }
 
 static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num_layers,
@@ -231,12 +233,14 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
     return BC_ERR_ARG;
   const bool state = h0 || c0 || hT || cT;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  hipStream_t st = S(stream);
+  int* call_status = reinterpret_cast<int*>(workspace);  // workspace[0]: this call's timeout count
+  if (hipMemsetAsync(call_status, 0, sizeof(int), st) != hipSuccess) return BC_ERR_LAUNCH;
   if (B == 0 || T == 0) return BC_OK;
   mode = lstm_mode(mode);
-  hipStream_t st = S(stream);
   const long long tb = (long long)T * B;
   if (tb > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
-  float* xt = workspace;
+  float* xt = workspace + LSTM_WS_STATUS_FLOATS;
   float* gx = xt + tb * H;
   float* ya = gx + tb * 4 * H;
   float* yb = ya + tb * H;
@@ -264,7 +268,7 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
       const long long so = (long long)l * H * B;  // layer l's [H][B] state
       rc = lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(w_hh_packed[l]), lout, cst, H, T, B,
                            mode == 3 ? 2 : 3, st, h0 ? h0 + so : nullptr, c0 ? c0 + so : nullptr,
-                           hT ? hT + so : nullptr, cT ? cT + so : nullptr);
+                           hT ? hT + so : nullptr, cT ? cT + so : nullptr, call_status);
       if (rc) return rc;
       lin = lout;
       lout = (lout == ya) ? yb : ya;
@@ -352,6 +356,11 @@ int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int 
                       void* stream) {
   if (!y || !skip || !out || B < 0 || C < 0 || T < 0) return BC_ERR_ARG;
   return ctb_to_btc_add_launch(y, skip, nullptr, nullptr, out, B, C, T, S(stream));
+}
+
+int bc_tanh_fwd(const float* x, float* y, long long n, void* stream) {
+  if (!x || !y || n < 0) return BC_ERR_ARG;
+  return tanh_launch(x, y, n, S(stream));
 }
 
 int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream) {

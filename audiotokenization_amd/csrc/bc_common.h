@@ -20,6 +20,14 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
     if (_e != hipSuccess) return BC_ERR_LAUNCH;             \
   } while (0)
 
+// Ablation switches (tools/*_ablation.sh timing experiments that deliberately skip work) exist only in
+// builds with -DBC_ABLATION; in the product library BC_ABL is the constant 0 and the branches vanish.
+#ifdef BC_ABLATION
+#define BC_ABL(flags, bit) ((flags) & (bit))
+#else
+#define BC_ABL(flags, bit) 0
+#endif
+
 namespace bc {
 
 // sin(x) for the Snake: Cody-Waite reduction by pi in 4 fma steps (valid for |x| < 39000), odd

@@ -57,6 +57,7 @@ int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t
 int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, const float* sb,
                           float* out, int B, int C, int T, hipStream_t st);
 int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st);
+int tanh_launch(const float* x, float* y, long long n, hipStream_t st);
 
 bool lstm_fast_ok(int H);
 void lstm_pack_hh2(const float* w, float* out, int H);
@@ -69,7 +70,8 @@ void lstm_seq_pack(const float* w, unsigned short* out, int H, int planes);
 long long lstm_seq_workspace_bytes(int H, int T);
 int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
                     int planes, hipStream_t st, const float* h0 = nullptr, const float* c0 = nullptr,
-                    float* hT = nullptr, float* cT = nullptr);
+                    float* hT = nullptr, float* cT = nullptr,
+                    int* call_status = nullptr);
 int lstm_seq_read_status(int reset);
 int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, int H, int B,
                      int T, int t, hipStream_t st);

@@ -266,14 +266,14 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     float bw0[CI], bw1[CI];
     if (a.nchunks > 1) load_b(1, bw0, bw1);
     auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
-      if (c + 1 < a.nchunks && !(a.dbg & 1)) issue_a(c + 1, (c + 1) & 1);
-      if (c + 2 < a.nchunks && !(a.dbg & 2)) load_b(c + 2, p0v, p1v);
+      if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
+      if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) load_b(c + 2, p0v, p1v);
       compute(c & 1, 0, 0);
       if (c + 1 < a.nchunks) {
         if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
         if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-        if (!(a.dbg & 4)) store_b(n0v, n1v);
+        if (!BC_ABL(a.dbg, 4)) store_b(n0v, n1v);
       }
       // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
       if (c + 2 < a.nchunks)
@@ -287,12 +287,12 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
     }
   } else {
-    const bool prio = a.dbg & 16;
+    const bool prio = BC_ABL(a.dbg, 16);
     for (int c = 0; c < a.nchunks; ++c) {
       for (int tp = 0; tp < kst; ++tp) {
         const int step = c * kst + tp;
-        if (step + 1 < nsteps && !(a.dbg & 1)) issue_a(step + 1, (step + 1) & 1);
-        if (tp == 0 && c + 1 < a.nchunks && !(a.dbg & 2)) load_b(c + 1, bv0, bv1);
+        if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
+        if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) load_b(c + 1, bv0, bv1);
         if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int tt = 0; tt < TPS; ++tt) {
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
           if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
           if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-          if (!(a.dbg & 4)) store_b(bv0, bv1);
+          if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
         // step 0 of a multi-step chunk the 2*CI B loads of the next chunk were issued after it and
@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     }
   }
 
-  if (!(a.dbg & 8)) {
+  if (!BC_ABL(a.dbg, 8)) {
     if constexpr (P == 2)
       conv_epilogue<MT, NT, true>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
     else

@@ -148,6 +148,13 @@ __global__ void __launch_bounds__(256) ctb_to_btc_add_kernel(const float* __rest
   }
 }
 
+// nn.Tanh (codec_decoder.py:80) as a standalone module call (decoder.model run as the reference's
+// nn.Sequential); inside decode() it is the last conv's epilogue (same tanhf).
+__global__ void tanh_kernel(const float* __restrict__ x, float* __restrict__ y, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = tanhf(x[i]);
+}
+
 // Clip i, sample n: u = (splitmix64(0xB16C0DEC ^ (i<<32) ^ n) >> 40) * 2^-24, x = u - 0.5.
 __global__ void synth_clips_kernel(float* __restrict__ x, int B, long long T, long long clip0) {
   const long long total = (long long)B * T;
@@ -203,6 +210,13 @@ int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, co
   if ((long long)B * C * T == 0) return BC_OK;
   dim3 grid((T + 31) / 32, C, (B + 63) / 64);
   hipLaunchKernelGGL(ctb_to_btc_add_kernel, grid, dim3(256), 0, st, y, skip, sa, sb, out, B, C, T);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int tanh_launch(const float* x, float* y, long long n, hipStream_t st) {
+  if (n == 0) return BC_OK;
+  hipLaunchKernelGGL(tanh_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, x, y, n);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

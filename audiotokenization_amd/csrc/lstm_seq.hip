@@ -59,7 +59,9 @@ struct LstmSeqArgs {
   float* y;                   // [H][T*Btot] output h_t (ctb layout)
   float* hseq;                // [T][H/32][4][64][8] fp32: h_t in MFMA-fragment order, one slot per step
   unsigned* flags;            // [G], zero before the launch
-  int* status;                // timeout counter (0 = ok)
+  int* status;                // this call's timeout counter (0 = ok), zeroed by the caller on the stream
+  int* status_total;          // process-wide diagnostic counter (bc_lstm_status)
+  unsigned spin_limit;        // polls before a workgroup gives up (LS_SPIN_LIMIT; tests force a small one)
   int H, T, Btot, b0, nb;
   int dbg;  // timing experiments only (BC_LSTM_SEQ_DEBUG): 4 = skip the flag poll (wrong results)
   long long* stamps;  // diagnostic s_memtime stamps (BC_LSTM_SEQ_STAMPS), nullptr in normal runs
@@ -186,13 +188,14 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
       // wait until the producers of h_{t-1}[my K range] have published step t-1
       const int p0 = w * nprod;
       unsigned spins = 0;
-      while (!(a.dbg & 4)) {
+      while (!BC_ABL(a.dbg, 4)) {
         const unsigned f = lane < nprod ? __hip_atomic_load(flags + p0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                         : 0xffffffffu;
         if (__all(f >= (unsigned)t)) break;
-        if (++spins > LS_SPIN_LIMIT) {
+        if (++spins > a.spin_limit) {
           if (lane == 0) {
             atomicAdd(a.status, 1);
+            atomicAdd(a.status_total, 1);
             bail = 1;
           }
           break;
@@ -446,13 +449,14 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
       if (t + sh > 0) {
         const ls_gu32* fl = flags + h * 256 + w * nprod;
         unsigned spins = 0;
-        while (!(a.dbg & 4)) {
+        while (!BC_ABL(a.dbg, 4)) {
           const unsigned f = lane < nprod ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                           : 0xffffffffu;
           if (__all(f >= (unsigned)(t + sh))) break;
-          if (++spins > LS_SPIN_LIMIT) {
+          if (++spins > a.spin_limit) {
             if (lane == 0) {
               atomicAdd(a.status, 1);
+              atomicAdd(a.status_total, 1);
               bail = 1;
             }
             break;
@@ -679,6 +683,8 @@ static long long* lstm_seq_stamp_buffer() {
   return p;
 }
 
+static unsigned g_spin_limit = LS_SPIN_LIMIT;
+
 static int device_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -689,8 +695,34 @@ static int device_cus() {
   return n;
 }
 
+// Every workgroup of a persistent launch must be resident at once (they wait on each other's flags):
+// G <= CUs x the kernel's occupancy per CU at 256 threads (its registers / LDS), checked per kernel.
+template <typename K>
+static bool all_resident(K kernel, int G) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess) return false;
+  return per_cu >= 1 && (long long)G <= (long long)per_cu * device_cus();
+}
+
+static bool seq_resident(int KS, int planes, bool halves, int G) {
+#define BC_LS_RES(K)                                                                        \
+  case K:                                                                                   \
+    if (planes == 2) return all_resident(lstm_seq2_x6_kernel<K, 2>, G);                     \
+    if (halves) return all_resident(lstm_seq2_x6_kernel<K, 3>, G);                          \
+    return all_resident(lstm_seq_x6_kernel<K>, G);
+  switch (KS) {
+    BC_LS_RES(2)
+    BC_LS_RES(4)
+    BC_LS_RES(8)
+    BC_LS_RES(12)
+    default: return false;
+  }
+#undef BC_LS_RES
+}
+
 int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* ws, int H, int T, int Btot,
-                    int planes, hipStream_t st, const float* h0, const float* c0, float* hT, float* cT) {
+                    int planes, hipStream_t st, const float* h0, const float* c0, float* hT, float* cT,
+                    int* call_status) {
   if (planes != 2 && planes != 3) return BC_ERR_ARG;
   if (!lstm_seq_ok(H)) return BC_ERR_UNSUPPORTED;
   const int G = H / LS_U;
@@ -703,7 +735,9 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
   a.y = y;
   a.flags = reinterpret_cast<unsigned*>(ws);
   a.hseq = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + LS_FLAG_BYTES);
-  a.status = status;
+  a.status = call_status ? call_status : status;
+  a.status_total = status;
+  a.spin_limit = g_spin_limit;
   a.H = H;
   a.T = T;
   a.Btot = Btot;
@@ -723,6 +757,11 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
     return !(e && atoi(e) == 1);
   }();
   if (!halves && (h0 || c0 || hT || cT)) return BC_ERR_UNSUPPORTED;  // carried state: lstm_seq2 only
+  static int resident_checked[4][2] = {};  // per (H/128 case, kernel): 1 ok, -1 refused
+  const int ks_idx = H == 256 ? 0 : H == 512 ? 1 : H == 1024 ? 2 : 3;
+  int& rs = resident_checked[ks_idx][planes == 2 ? 0 : 1];
+  if (rs == 0) rs = seq_resident(H / 128, planes, halves, G) ? 1 : -1;
+  if (rs < 0) return BC_ERR_UNSUPPORTED;
   for (int b0 = 0; b0 < Btot; b0 += LS_NB) {
     a.b0 = b0;
     a.nb = Btot - b0 < LS_NB ? Btot - b0 : LS_NB;
@@ -750,6 +789,14 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
 }
 
 }  // namespace bc
+
+// Diagnostics only (not part of include/bigcodec.h): override the persistent kernel's poll limit
+// (limit 0 = restore the default).  Tests force the timeout path with a tiny limit.
+extern "C" int bc_debug_set_lstm_spin_limit(long long limit) {
+  if (limit < 0 || limit > 0xffffffffLL) return 1;
+  bc::g_spin_limit = limit == 0 ? bc::LS_SPIN_LIMIT : (unsigned)limit;
+  return 0;
+}
 
 // Diagnostics only (not part of include/bigcodec.h): copy the last persistent launch's stamps
 // [2 workgroups][2048 steps][4 waves][8 events] (s_memtime ticks) to the host; synchronises.

@@ -215,8 +215,8 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   for (int c = 0; c < a.nchunks; ++c) {
     for (int tp = 0; tp < kst; ++tp) {
       const int step = c * kst + tp;
-      if (step + 1 < nsteps && !(r.dbg & 1)) issue_a(a.w, step + 1, (step + 1) & 1);
-      if (tp == 0 && c + 1 < a.nchunks && !(r.dbg & 2)) load_b(c + 1);
+      if (step + 1 < nsteps && !BC_ABL(r.dbg, 1)) issue_a(a.w, step + 1, (step + 1) & 1);
+      if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(r.dbg, 2)) load_b(c + 1);
 #pragma unroll
       for (int tt = 0; tt < TPS; ++tt) {
       const int tap = tp * TPS + tt;
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
   // ---------------- phase 2: y = conv1(h_act), input as the MFMA A operand ----------------
   // Wave (mq, jg) computes m-tile mq for n-tiles [jg * NTW, (jg + 1) * NTW) from its register-resident
   // k=1 weights; Hs is read-only here, so phase 2 runs without a barrier.
-  if (p2 && !(r.dbg & 8)) {
+  if (p2 && !BC_ABL(r.dbg, 8)) {
     floatx4 acc2[1][NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc2[0][j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
         }
       }
     }
-    if (r.dbg & 4) {
+    if (BC_ABL(r.dbg, 4)) {
       if (acc2[0][0][0] == 1234.5f) e.y[0] = 0.f;  // keep the MFMAs alive
     } else {
       conv_epilogue<1, NTW, P == 2>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs);

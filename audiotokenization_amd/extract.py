@@ -126,48 +126,121 @@ def all_gather_codes(codes: torch.Tensor, group=None) -> torch.Tensor:
     return out.view((world,) + tuple(codes.shape))
 
 
+def all_gather_status(status: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather a small int64 status vector per rank -> (W, n)."""
+    import torch.distributed as dist
+
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return status.unsqueeze(0)
+    world = dist.get_world_size(group)
+    out = torch.empty((world * status.numel(),), dtype=status.dtype, device=status.device)
+    dist.all_gather_into_tensor(out, status.contiguous(), group=group)
+    return out.view(world, status.numel())
+
+
 @dataclass
 class ExtractStats:
-    clips: int = 0
-    errors: int = 0
+    clips: int = 0          # this rank's clips encoded
+    errors: int = 0         # this rank's clips lost to a failed batch (extract_indices.py:565-574)
     frames: int = 0
+    batches: int = 0
     error_items: List[int] = field(default_factory=list)
+    job_errors: int = 0     # clips lost on ANY rank (every rank sees the per-batch status gather)
+    job_clips: int = 0      # clips encoded on all ranks
 
 
-def extract_sharded(model: BigCodecModel, n_clips: int, n_samples: int, batch: int, rank: int = 0,
-                    world: int = 1, device=None, gather: bool = True, sink=None, group=None) -> ExtractStats:
-    """Encode clips [0, n_clips) clip-sharded over `world` ranks (synthetic corpus, config 4).
+def _codes_of(out) -> torch.Tensor:
+    return out["indices"] if isinstance(out, dict) else out
 
-    Every rank runs the same number of batches (the last one padded with clip ids that are
-    discarded) so the per-batch all-gather lines up.  `sink(global_clip_ids, codes_np)` receives the
-    gathered (n, F, Nq) int16 arrays on rank 0 (e.g. an .npy writer)."""
-    device = device or torch.device("cuda", torch.cuda.current_device())
-    lo, hi = shard_range(n_clips, rank, world)
-    per_rank = max(shard_range(n_clips, r, world)[1] - shard_range(n_clips, r, world)[0] for r in range(world))
-    n_batches = (per_rank + batch - 1) // batch
-    stats = ExtractStats()
-    for bi in range(n_batches):
-        s = lo + bi * batch
-        e = min(s + batch, hi)
-        real = max(0, e - s)
-        x = synth_batch(batch, n_samples, s, device)
+
+class ShardedExtractor:
+    """Clip-sharded extraction of clips [0, n_clips) over `world` ranks.
+
+    Rank r owns the block shard_range(n_clips, r, world) and walks it in batches of `batch`; every
+    rank runs the same number of batches (the last ones padded with clip ids that are discarded), so
+    the per-batch collectives line up.  A batch whose source or model raises is counted, not fatal
+    (extract_indices.py:565-574) — and the failing rank STILL joins both of the batch's collectives:
+    first an all-gather of (ok, Nq, F) per rank, then, if any rank succeeded, the all-gather of the
+    (Nq, B, F) codes, in which a failed rank contributes zeros of the agreed shape.  No rank can be
+    left waiting in a collective another rank skipped.
+
+    `source(clip0, n) -> (n, 1, T)` supplies a batch (default: bc_synth_clips on `device`);
+    `model(x)` returns the codes (Nq, B, F) or a dict with "indices" (BigCodecModel);
+    `sink(global_clip_id, codes (F, Nq) int16)` receives every successfully encoded clip of the job
+    on rank 0 (e.g. an .npy writer, save_indices)."""
+
+    def __init__(self, model, n_clips: int, n_samples: int, batch: int, rank: int = 0, world: int = 1,
+                 device=None, gather: bool = True, sink=None, group=None, source=None):
+        if batch <= 0 or n_clips < 0:
+            raise ValueError("batch must be > 0 and n_clips >= 0")
+        self.model, self.n_clips, self.n_samples, self.batch = model, n_clips, n_samples, batch
+        self.rank, self.world, self.gather, self.sink, self.group = rank, world, gather, sink, group
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.source = source or (lambda clip0, n: synth_batch(n, n_samples, clip0, self.device))
+        self.lo, self.hi = shard_range(n_clips, rank, world)
+        per_rank = max(shard_range(n_clips, r, world)[1] - shard_range(n_clips, r, world)[0] for r in range(world))
+        self.n_batches = (per_rank + batch - 1) // batch
+        self.stats = ExtractStats()
+        self.last = None  # rank 0: the last batch's gathered (W, B, F, Nq) int16 host array
+
+    def step(self, bi: int):
+        """Batch `bi` of every rank: encode, gather, hand to the sink.  Returns the gathered
+        (W, Nq, B, F) device codes, or None when the batch failed on every rank."""
+        st = self.stats
+        s = self.lo + bi * self.batch
+        real = max(0, min(s + self.batch, self.hi) - s)
+        codes = None
         try:
-            codes = model(x)["indices"]
+            codes = _codes_of(self.model(self.source(s, self.batch)))
+            if codes.ndim != 3 or codes.shape[1] != self.batch:
+                raise ValueError(f"model returned codes of shape {tuple(codes.shape)}, expected (Nq, {self.batch}, F)")
         except Exception:  # per-batch accounting, mirrors extract_indices.py:565-574
-            stats.errors += real
-            stats.error_items.extend(range(s, e))
             codes = None
+            st.errors += real
+            st.error_items.extend(range(s, s + real))
+        st.batches += 1
+        if codes is not None:
+            st.clips += real
+            st.frames += real * codes.shape[-1]
+        gather = self.gather and self.world > 1
+        dev = codes.device if codes is not None else self.device
+        status = torch.tensor([1 if codes is not None else 0, codes.shape[0] if codes is not None else 0,
+                               codes.shape[2] if codes is not None else 0, real], dtype=torch.int64)
+        stat = all_gather_status(status.to(dev), self.group).cpu() if gather else status.unsqueeze(0)
+        ok = stat[:, 0].bool()
+        st.job_errors += int(stat[~ok, 3].sum())
+        st.job_clips += int(stat[ok, 3].sum())
+        if not bool(ok.any()):
+            return None
+        first = int(torch.nonzero(ok)[0, 0])
+        nq, nf = int(stat[first, 1]), int(stat[first, 2])
         if codes is None:
-            continue
-        stats.clips += real
-        stats.frames += real * codes.shape[-1]
-        gathered = all_gather_codes(codes, group) if gather else codes.unsqueeze(0)
-        if sink is not None and rank == 0:
+            codes = torch.zeros((nq, self.batch, nf), dtype=torch.int64, device=dev)
+        elif (codes.shape[0], codes.shape[2]) != (nq, nf):
+            raise RuntimeError(f"rank {self.rank}: codes {tuple(codes.shape)} disagree with rank {first}'s "
+                               f"(Nq={nq}, F={nf}); every rank must encode the same clip length")
+        gathered = all_gather_codes(codes, self.group) if gather else codes.unsqueeze(0)
+        if self.rank == 0 and self.sink is not None:
             arr = gathered.permute(0, 2, 3, 1).cpu().numpy().astype(np.int16)  # (W, B, F, Nq)
-            for r in range(gathered.shape[0]):
-                rlo, rhi = shard_range(n_clips, r, world) if gather else (lo, hi)
-                rs = rlo + bi * batch
-                for j in range(batch):
+            self.last = arr
+            for r in range(arr.shape[0]):
+                if not bool(ok[r]):
+                    continue
+                rlo, rhi = shard_range(self.n_clips, r, self.world) if gather else (self.lo, self.hi)
+                rs = rlo + bi * self.batch
+                for j in range(self.batch):
                     if rs + j < rhi:
-                        sink(rs + j, arr[r, j])
-    return stats
+                        self.sink(rs + j, arr[r, j])
+        return gathered
+
+    def run(self) -> ExtractStats:
+        for bi in range(self.n_batches):
+            self.step(bi)
+        return self.stats
+
+
+def extract_sharded(model, n_clips: int, n_samples: int, batch: int, rank: int = 0, world: int = 1, device=None,
+                    gather: bool = True, sink=None, group=None, source=None) -> ExtractStats:
+    """Encode clips [0, n_clips) clip-sharded over `world` ranks (ShardedExtractor.run)."""
+    return ShardedExtractor(model, n_clips, n_samples, batch, rank, world, device, gather, sink, group,
+                            source).run()

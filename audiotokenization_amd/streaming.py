@@ -22,6 +22,7 @@ from typing import Dict, Optional
 
 import torch
 
+from . import _lib
 from .blocks import EncoderBlock, ResLSTM, _conv_of
 from .modules import _as_input
 
@@ -86,7 +87,9 @@ class StreamingEncoder:
             else:
                 raise NotImplementedError(f"unexpected encoder stage {type(st).__name__}")
         self.samples += x.shape[-1]
-        return self._conv(last_conv, final_act(h))
+        out = self._conv(last_conv, final_act(h))
+        _lib.check_status()
+        return out
 
     def encode(self, x, chunk: int) -> torch.Tensor:
         """Whole input through `push` in chunks of `chunk` samples (the last may be shorter)."""

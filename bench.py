@@ -2,24 +2,31 @@
 
 Default (what the driver runs) = BASELINE config 2: batch = 64 x 10 s @24 kHz clips per GPU, encode +
 VQ (the extract_indices.py path: encoder -> decoder(vq=True) -> codes) of the `default` BigCodec
-model, fp32-accurate arithmetic, synthetic white-noise clips already resident in HBM, random
+model, fp32-class arithmetic (h3), synthetic white-noise clips already resident in HBM, random
 (counter-hash) weights.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--precision fp32|x6|bf16]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6] [--precision h3|x6|fp32|bf16]
+
+--gpus N > 1 starts N ranks itself (python -m torch.distributed.run as a child process, before this
+process touches the GPU); under torchrun WORLD_SIZE must equal --gpus.  One process per GPU, RCCL.
 
 --config 3: full encode -> VQ -> decode round trip (inference_full.py's model path), parity adds the
             decoder's waveform error against the CPU oracle decoding the same codes.
---config 4: extract_indices-style corpus streaming: every step synthesises the rank's NEXT batch of
-            clips on the device, encodes + quantises it, all-gathers the indices (RCCL) and copies
-            them to the host as int16 (the .npy payload).
+--config 4: extract_indices-style corpus streaming through extract.ShardedExtractor (the product's
+            extract_sharded loop): every step is every rank's NEXT batch of a 100 k-clip corpus,
+            synthesised on the device, encoded + quantised, its indices all-gathered (RCCL), and
+            rank 0's sink receives every clip's int16 (F, Nq) .npy payload.
 --config 5: batch = 32 x 30 s per GPU with bf16 conv products (precision 'bf16'); parity reports the
             index mismatch rate against the fp32-accurate path on the same batch.
+--config 6: token -> audio decode (tokens.py service path).
 
 A step = one batch per GPU through the path; for N > 1 each step ends with the RCCL all-gather of the
 batch's index tensor (clip-sharded data parallelism, weak scaling).  Rank 0 prints one JSON line with
 the whole-job throughput (audio-seconds per second, all GPUs), the roofline of the dominant kernel
-(HIP-event timed inside the timed region) and the CPU oracle baseline.
+(HIP-event timed inside the timed region), the CPU oracle baseline, the index parity of rank 0's batch
+against the reference's full-size fixture (tests/golden/full_config2_default.npz: every mismatch with
+its fp64 top-2 gap) and, for config 2, the same workload in the exact x6 arithmetic beside the h3
+headline.
 """
 from __future__ import annotations
 
@@ -100,7 +107,11 @@ def parse():
     p.add_argument("--sample-rate", type=int, default=24000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true")
-    p.add_argument("--cpu-clips", type=int, default=4, help="clips in the CPU-baseline sample (about 3 s each)")
+    p.add_argument("--cpu-clips", type=int, default=4, help="clips in the CPU-baseline B=1 sample (about 3 s each)")
+    p.add_argument("--cpu-batches", default="4,16", help="batch sizes of the extra CPU-baseline calls ('' = none)")
+    p.add_argument("--no-x6", action="store_true", help="skip the fp32-accurate x6 leg beside the h3 headline")
+    p.add_argument("--x6-steps", type=int, default=2)
+    p.add_argument("--corpus", type=int, default=100_000, help="config 4: clips in the synthetic corpus")
     p.add_argument("--precision", choices=["fp32", "x6", "bf16", "h3"], default=None,
                    help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or h3)")
     a = p.parse_args()
@@ -165,46 +176,136 @@ def mfma_probe_tflops(dev, nwg=2048, iters=60000):
     return nwg * 4 * iters * 16 * 16384.0 / (e0.elapsed_time(e1) * 1e-3) / 1e12
 
 
-def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False):
+def cpu_info():
+    """(threads to use, description): the physical cores this process may run on — the affinity set
+    mapped to (package, core) pairs via /proc/cpuinfo, capped by a cgroup CPU quota (cpu.max) when one
+    is set — and the CPU model name."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    model, cores, cur = None, set(), {}
+    try:
+        for line in open("/proc/cpuinfo").read().split("\n") + [""]:
+            if not line.strip():
+                if cur.get("processor") is not None and int(cur["processor"]) in aff:
+                    cores.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                cur = {}
+                continue
+            k, _, v = line.partition(":")
+            cur[k.strip()] = v.strip()
+            if k.strip() == "model name" and model is None:
+                model = v.strip()
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    phys = len(cores) or len(aff)
+    threads = max(1, min(phys, quota or phys))
+    desc = (f"{model or 'unknown CPU'}; {len(aff)} logical CPUs in affinity = {phys} physical cores"
+            + (f", cgroup quota {quota} CPUs" if quota else ", no cgroup CPU quota") + f" -> {threads} threads")
+    return threads, desc
+
+
+def cpu_baseline(name, n_samples, sds, ek, dk, n_clips, roundtrip=False, batches=(1, 4, 16)):
     """The CPU oracle (torch CPU restatement, bit-identical to the reference in the development
-    container) timed on this host: encode + VQ (+ decode for the round trip), B = 1 per clip
-    (extract_indices.py:397), warm run.  Returns (baseline dict, codes, waveforms or None)."""
+    container) timed on this host with every physical core available to the process:
+    encode + VQ (+ decode for the round trip), B = 1 per clip (extract_indices.py:397) over `n_clips`
+    clips, plus one call of each batch size in `batches` > 1 (best of B in {1, 4, 16}), warm.
+    Returns (baseline dict, codes (Nq, n_clips, F), embeddings, waveforms or None)."""
     import torch
 
     from audiotokenization_amd import synth
     from oracle import bigcodec_oracle as O
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    threads, desc = cpu_info()
     torch.set_num_threads(threads)
-    x = torch.from_numpy(synth.synth_clips(n_clips, n_samples, clip0=0)).unsqueeze(1)
-    codes, wavs = [], []
+    nb = max([n_clips] + [b for b in batches if not roundtrip])
+    x = torch.from_numpy(synth.synth_clips(nb, n_samples, clip0=0)).unsqueeze(1)
+    codes, embs, wavs = [], [], []
     with torch.no_grad():
         O.encode_indices(x[:1, :, : n_samples // 10], sds[0], sds[1], ek, dk)  # warm-up (short)
         t0 = time.perf_counter()
         for i in range(n_clips):
             c, emb = O.encode_indices(x[i:i + 1], sds[0], sds[1], ek, dk)
             codes.append(c)
+            embs.append(emb)
             if roundtrip:
                 zq, _, _ = O.rvq_forward(emb, sds[1], "quantizer.", dk.get("vq_num_quantizers", 1))
                 wavs.append(O.decoder_forward(zq, sds[1], dk))
         dt = time.perf_counter() - t0
-        # SURVEY §8(d): also the batched CPU rate (the same clips as one B = n_clips call); best of both
-        dtb = None
-        if not roundtrip and n_clips > 1:
-            t0 = time.perf_counter()
-            O.encode_indices(x, sds[0], sds[1], ek, dk)
-            dtb = time.perf_counter() - t0
-    audio_s = n_clips * n_samples / 24000.0
+        rates = {"B=1": n_clips * n_samples / 24000.0 / dt}
+        total = dt
+        if not roundtrip:
+            for b in batches:
+                if b <= 1:
+                    continue
+                t0 = time.perf_counter()
+                O.encode_indices(x[:b], sds[0], sds[1], ek, dk)
+                tb = time.perf_counter() - t0
+                total += tb
+                rates[f"B={b}"] = b * n_samples / 24000.0 / tb
     what = "encode+VQ+decode" if roundtrip else "encode+VQ"
-    rates = {"B=1": audio_s / dt}
-    if dtb:
-        rates[f"B={n_clips}"] = audio_s / dtb
     best = max(rates, key=rates.get)
-    return (dict(value=rates[best], unit="audio-sec/s", cores=threads, kind="port", rates=rates,
-                 sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz, {name} model, {what}, best of "
-                        f"{'/'.join(rates)} ({best}; B=1 is extract_indices.py:397), torch CPU oracle, "
-                        f"{dt + (dtb or 0):.1f} s"),
-            torch.cat(codes, dim=1), torch.cat(wavs, dim=0) if roundtrip else None)
+    return (dict(value=rates[best], unit="audio-sec/s", cores=threads, kind="port", rates=rates, cpu=desc,
+                 b1_value=rates["B=1"],
+                 sample=f"{n_clips} clip(s) x {n_samples / 24000:.0f} s @24 kHz at B=1"
+                        + "".join(f", 1 call at {k}" for k in rates if k != "B=1")
+                        + f"; {name} model, {what}, torch CPU oracle (bit-identical to the reference in the "
+                          f"development container), best = {best} (B=1 is extract_indices.py:397), {total:.1f} s"),
+            torch.cat(codes, dim=1), torch.cat(embs, dim=0), torch.cat(wavs, dim=0) if roundtrip else None)
+
+
+def vq_gaps(emb, dec_sd):
+    """fp64 top-2 distance gap of every frame of the oracle's latent (the certificate of a flip)."""
+    import torch
+
+    from oracle import bigcodec_oracle as O
+
+    z_e = O.fvq_forward(emb, dec_sd, "quantizer.layers.0.", return_ze=True)[3]
+    b, d, t = z_e.shape
+    e = z_e.permute(0, 2, 1).reshape(-1, d).double()
+    e = e / e.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    c = dec_sd["quantizer.layers.0._codebook.weight"].double()
+    c = c / c.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    dist = (e * e).sum(1, keepdim=True) - 2 * e @ c.t() + (c * c).sum(1)[None]
+    v, _ = torch.topk(dist, 2, dim=1, largest=False)
+    return (v[:, 1] - v[:, 0]).reshape(b, t).numpy()
+
+
+GAP_TOL = 1e-6  # a flip is certified only at a frame whose fp64 top-2 gap is below this (tests/helpers.py)
+
+
+def mismatch_report(got, want, gap, reference):
+    """Every index mismatch with its certified fp64 top-2 gap."""
+    import numpy as np
+
+    got = np.asarray(got).reshape(want.shape)
+    bad = np.argwhere(got != want)
+    items = [{"clip": int(b), "frame": int(f), "got": int(got[b, f]), "want": int(want[b, f]),
+              "gap": float(gap[b, f])} for b, f in bad[:64]]
+    worst = max((float(gap[b, f]) for b, f in bad), default=0.0)
+    return {"reference": reference, "frames": int(want.size), "index_mismatches": int(len(bad)),
+            "mismatches": items, "worst_gap": worst, "gap_tol": GAP_TOL, "all_certified": worst <= GAP_TOL,
+            "min_gap_all_frames": float(np.min(gap))}
+
+
+def golden_parity(codes, model, n_samples, B):
+    """Rank 0's batch (clips 0..B-1) against tests/golden/full_config2_default.npz: the REFERENCE's
+    indices for clips 0..63 x 240 000 samples of the default model (tools/make_golden_full.py), every
+    mismatch listed with its fp64 top-2 gap.  None when the workload is not that fixture's."""
+    import numpy as np
+
+    path = os.path.join(REPO, "tests", "golden", "full_config2_default.npz")
+    if model != "default" or n_samples != 240_000 or not os.path.exists(path):
+        return None
+    g = np.load(path)
+    n = min(B, g["codes"].shape[0])
+    got = codes[0, :n].cpu().numpy()
+    return mismatch_report(got, g["codes"][:n].astype(np.int64), g["gap"][:n],
+                           f"reference CPU path (tests/golden/full_config2_default.npz, clips 0-{n - 1})")
 
 
 def cpu_decode_baseline(codes, sds, dk, n_clips):
@@ -215,7 +316,7 @@ def cpu_decode_baseline(codes, sds, dk, n_clips):
 
     from oracle import bigcodec_oracle as O
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    threads, desc = cpu_info()
     torch.set_num_threads(threads)
     nq = codes.shape[2]
     with torch.no_grad():
@@ -227,14 +328,39 @@ def cpu_decode_baseline(codes, sds, dk, n_clips):
             wavs.append(O.decoder_forward(emb.transpose(1, 2).contiguous(), sds[1], dk))
         dt = time.perf_counter() - t0
     audio_s = n_clips * codes.shape[1] * int(np.prod(dk["up_ratios"])) / 24000.0
-    return (dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port",
+    return (dict(value=audio_s / dt, unit="audio-sec/s", cores=threads, kind="port", cpu=desc,
                  sample=f"{n_clips} clip(s) x {codes.shape[1]} frames, token -> audio decode, B=1, torch CPU "
                         f"oracle, {dt:.1f} s"),
             torch.cat(wavs, dim=0))
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed environment: start N ranks as CHILD processes
+    (python -m torch.distributed.run ...) before this process touches the GPU, and exit with their
+    code.  Under a launcher, WORLD_SIZE must equal --gpus."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={env_world} disagrees with --gpus {args.gpus}")
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
     args = parse()
+    launch_ranks(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -248,7 +374,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from audiotokenization_amd import _lib
-    from audiotokenization_amd.extract import all_gather_codes, batch_indices_to_numpy, synth_batch
+    from audiotokenization_amd.extract import ShardedExtractor, all_gather_codes, synth_batch
 
     _lib.load()
     if args.precision:
@@ -259,13 +385,21 @@ def main():
     B = args.batch
     cfgn = args.config
     x = synth_batch(B, n_samples, clip0=rank * B, device=dev)  # resident in HBM before timing
-    state = {"batch": 0, "wav": None, "host": None}
+    state = {"wav": None, "host": 0}
     tok = None
     if cfgn == 6:  # synthetic codes of the clips' frame count, uniform over the codebook, seeded per rank
         n_frames = n_samples // int(dec.hop_length)
         g = torch.Generator().manual_seed(1234 + rank)
         tok = torch.randint(0, dec.quantizer.layers[0].codebook_size, (B, n_frames, 1), generator=g)
         tok_dev = tok.to(dev)
+    extractor = None
+    if cfgn == 4:  # the 100 k-clip corpus, clip-sharded; every step is the next batch of every rank
+        def sink(cid, arr):  # rank 0 receives every clip's (F, Nq) int16 .npy payload (file writes excluded)
+            state["host"] += 1
+
+        extractor = ShardedExtractor(lambda xb: dec(enc(xb), vq=True)[1], args.corpus, n_samples, B, rank, world,
+                                     dev, sink=sink)
+        state["bi"] = 0
 
     def step():
         if cfgn == 6:
@@ -273,43 +407,45 @@ def main():
                 state["wav"] = dec.tokens_to_audio(tok_dev)
             return None
         with torch.no_grad():
-            xb = x
-            if cfgn == 4:  # the rank's next batch of the corpus, synthesised on the device
-                xb = synth_batch(B, n_samples, clip0=(state["batch"] * world + rank) * B, device=dev)
-                state["batch"] += 1
-            post, codes, _ = dec(enc(xb), vq=True)
+            if cfgn == 4:  # extract_sharded's loop body: synthesise, encode + VQ, gather, int16 host copy
+                codes = extractor.step(state["bi"])
+                state["bi"] += 1
+                return codes
+            post, codes, _ = dec(enc(x), vq=True)
             if cfgn == 3:
                 state["wav"] = dec(post, vq=False)
             if world > 1:
                 codes = all_gather_codes(codes)
-            if cfgn == 4:  # int16 payload of the .npy files, every rank's clips
-                c = codes if codes.ndim == 3 else codes.permute(1, 0, 2, 3).reshape(codes.shape[1], -1, codes.shape[3])
-                state["host"] = batch_indices_to_numpy(c)
         return codes
+
+    def timed(n_steps, timer=None):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        _lib.set_timer(timer)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            codes = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        _lib.set_timer(None)
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, codes
 
     for _ in range(args.warmup):
         codes = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    state["batch"] = 0
     timer = None if args.no_kernel_timer else _lib.KernelTimer()
-    _lib.set_timer(timer)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        codes = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    _lib.set_timer(None)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, codes = timed(args.steps, timer)
+    if cfgn == 4:
+        assert extractor.stats.errors == 0 and extractor.stats.job_errors == 0, extractor.stats
 
     audio_s = world * B * n_samples / args.sample_rate * args.steps
     value = audio_s / elapsed
@@ -341,6 +477,29 @@ def main():
                 "all_python_conv_tflops": round(sum(v["flops_total"] for v in summ.values()) / (conv_ms * 1e-3) / 1e12, 2),
                 "kernels_top": kernel_table(summ, args.steps, probe)}
 
+    # rank 0's own batch codes (Nq, B, F) of the last timed step, for parity
+    mine = None
+    if cfgn in (2, 3):
+        mine = (codes[0] if world > 1 else codes)[:, :B]
+    elif cfgn == 4:
+        with torch.no_grad():
+            mine = dec(enc(x), vq=True)[1]  # rank 0's batch 0 = clips 0..B-1 (block partition at rank 0)
+
+    # fp32-accurate x6 leg (exact 3 x bf16 split) beside the h3 headline: same workload, own timing
+    x6 = None
+    if cfgn == 2 and args.precision == "h3" and not args.no_x6:
+        _lib.set_precision("x6")
+        for _ in range(1):
+            step()
+        el6, codes6 = timed(args.x6_steps)
+        _lib.set_precision(args.precision)
+        v6 = world * B * n_samples / args.sample_rate * args.x6_steps / el6
+        x6 = {"precision": "x6: fp32 operands split exactly into 3 bf16 terms, 6 bf16 MFMAs per product, fp32 "
+                           "accumulate (24-bit operands)",
+              "value": round(v6, 2), "ms_per_step": round(el6 / args.x6_steps * 1e3, 2), "steps": args.x6_steps}
+        if rank == 0:
+            x6["parity"] = golden_parity((codes6[0] if world > 1 else codes6)[:, :B], args.model, n_samples, B)
+
     cpu = None
     parity = None
     if rank == 0 and cfgn == 5:
@@ -360,40 +519,49 @@ def main():
         parity = {"clips_checked": args.cpu_clips, "samples": int(r.numel()),
                   "waveform_mse": float(((w - r) ** 2).mean()), "waveform_max_abs": float((w - r).abs().max()),
                   "note": "same codes through the CPU oracle's vq2emb + decoder"}
-    if rank == 0 and not args.no_cpu_baseline and cfgn not in (5, 6):
-        cpu, codes_ref, wav_ref = cpu_baseline(args.model, n_samples, sds, ek, dk, args.cpu_clips,
-                                               roundtrip=cfgn == 3)
-        got = codes[0] if world > 1 else codes
-        if cfgn == 4:  # the last step's batch: recompute the first clip of rank 0's batch 0
-            with torch.no_grad():
-                got = dec(enc(x), vq=True)[1]
-        got = got[:, : args.cpu_clips].cpu()
-        parity = {"clips_checked": args.cpu_clips, "frames": int(got.numel()),
-                  "index_mismatches": int((got != codes_ref).sum())}
-        if cfgn == 3:
-            w = state["wav"][: args.cpu_clips].double().cpu()
-            r = wav_ref.double()
-            parity["waveform_mse"] = float(((w - r) ** 2).mean())
-            parity["waveform_max_abs"] = float((w - r).abs().max())
-            parity["note"] = "waveforms compared end to end; equal codes make it the decoder's error alone"
+    if rank == 0 and cfgn in (2, 3, 4):
+        parity = {}
+        full = golden_parity(mine, args.model, n_samples, B)
+        if full is not None:
+            parity["vs_reference_fixture"] = full
+        if not args.no_cpu_baseline:
+            batches = tuple(int(b) for b in args.cpu_batches.split(",")) if args.cpu_batches else ()
+            cpu, codes_ref, emb_ref, wav_ref = cpu_baseline(args.model, n_samples, sds, ek, dk, args.cpu_clips,
+                                                            roundtrip=cfgn == 3, batches=batches)
+            n = args.cpu_clips
+            parity["vs_cpu_oracle"] = mismatch_report(mine[0, :n].cpu().numpy(), codes_ref[0].numpy(),
+                                                      vq_gaps(emb_ref, sds[1]),
+                                                      f"CPU oracle run here on clips 0-{n - 1}")
+            if cfgn == 3:
+                w = state["wav"][:n].double().cpu()
+                r = wav_ref.double()
+                parity["waveform_mse"] = float(((w - r) ** 2).mean())
+                parity["waveform_max_abs"] = float((w - r).abs().max())
+                parity["note"] = "waveforms compared end to end; equal codes make it the decoder's error alone"
     if rank == 0:
-        dtype = {"fp32": "f32", "x6": "f32 (3xbf16-split MFMA, fp32 accumulate)",
-                 "h3": "f32 (2xfp16 block-scaled split MFMA, fp32 accumulate)",
-                 "bf16": "bf16 conv products, fp32 accumulate/storage (LSTM and VQ fp32-accurate)"}[args.precision]
-        if cfgn == 4 and state["host"] is not None:
-            assert state["host"].dtype == np.int16
+        prec = {"fp32": ("f32", "native fp32 MFMA (v_mfma_f32_16x16x4f32)"),
+                "x6": ("f32", "fp32-class: operands split exactly into 3 bf16 terms (24-bit), 6 bf16 MFMAs per "
+                              "product, fp32 accumulate"),
+                "h3": ("f32", "fp32-class: operands block-scaled and split into 2 fp16 terms (22-bit), 3 fp16 "
+                              "MFMAs per product (lo x lo dropped, < 2^-22 relative), fp32 accumulate"),
+                "bf16": ("bf16", "bf16 conv products (one bf16 MFMA per product), fp32 accumulate and storage; "
+                                 "LSTM and VQ fp32-accurate")}[args.precision]
         line = {
             "metric": METRIC_RT if cfgn == 3 else METRIC_DEC if cfgn == 6 else METRIC, "value": round(value, 2),
             "unit": "audio-sec/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": prec[0],
+            "precision": {"mode": args.precision, "arithmetic": prec[1]}, "data": "synthetic",
             "config": {"workload": f"config{cfgn}: batch={B} x {args.seconds:g} s {args.sample_rate // 1000} kHz "
                                    f"clips per GPU, {CONFIGS[cfgn]['work']}, BigCodec '{args.model}' model, "
-                                   f"random weights",
+                                   f"random weights" + (f", corpus of {args.corpus} clips" if cfgn == 4 else ""),
                        "global_batch": B * world, "clip_samples": n_samples, "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roof, "cpu_baseline": cpu, "parity": parity, "x6": x6,
         }
+        if cfgn == 4:
+            line["extract"] = {"batches_per_rank": args.steps, "clips_sunk_rank0": state["host"],
+                               "errors": extractor.stats.job_errors}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 7
+#define BC_ABI_VERSION 8
 
 int bc_abi_version(void);
 
@@ -45,6 +45,12 @@ int bc_abi_version(void);
  * the fp32 kernel's.  mode 2: plain bf16 products with fp32 accumulation (one MFMA
  * per pair; BASELINE config 5's "bf16 encoder conv stack"; activations stay fp32 in memory) where
  * Cin >= 16, else fp32.  bc_reslstm_fwd runs mode 2 as mode 1 (the recurrence stays fp32-accurate).
+ * mode 3 ("h3", the package default): fp32-class block-scaled 2 x fp16 split — each operand block is
+ * scaled by a power of two from its maximum (weights per output row, packed by bc_conv1d_pack;
+ * activations per staged 32-channel chunk) and split v*S = hi + lo (two fp16 terms, 22 significant
+ * bits); a*b accumulates hi*hi + hi*lo + lo*hi in fp32 on v_mfma_f32_16x16x32_f16 (the dropped lo*lo
+ * term is below 2^-22 |ab|), 3 MFMAs per pair, where Cin >= 16, else fp32.  Error against fp64 at or
+ * below the native fp32 kernel's.
  * out_snake_alpha_exp[c] = exp(alpha[c]); out_snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9).
  * Limits: Cin*Tin*4 < 2^31 bytes per clip. */
 int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode);
@@ -56,15 +62,16 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
                   int K, int stride, int dilation, int pad_left, int epilogue, int cfg,
                   void* stream);
 
-/* ---- ResidualUnit in one launch (mode 1 / x6 only) ---------------------------------------------
+/* ---- ResidualUnit in one launch (modes 1 "x6" and 3 "h3"; C in {16, 32, 48, 64, 96}) -------------
  * Replaces ResidualUnit.forward (vq/module.py:88-89) after its first Activation1d:
  *   v = x_raw + conv1(snake_mid(conv7_d(x_act)))      (x_act = snake1(x_raw), from the producer)
  *   y = v, or snake_out(v), or y = v and y2 = snake_out(v)  (epilogue as bc_conv1d_fwd)
  * x_raw, x_act, y, y2: [B][C][T]; the k=7 conv keeps length T (pad_left = 3*dilation non-causal,
  * 6*dilation causal; the rest on the right).  w7_packed / w1_packed = bc_conv1d_pack(folded weight,
  * K = 7 / 1, cfg) with cfg = bc_resunit_select_cfg(C, dilation, mode); that returns -1 where the
- * unit does not fit one workgroup (then run the two bc_conv1d_fwd calls).  The activated k=7 output
- * stays in LDS (never written to memory).  mid_snake_*: the unit's second Activation1d. */
+ * unit does not fit one workgroup, or mode is 0 / 2 (then run the two bc_conv1d_fwd calls).  The
+ * activated k=7 output stays in LDS (never written to memory).  mid_snake_*: the unit's second
+ * Activation1d. */
 int bc_resunit_select_cfg(int C, int dilation, int mode);
 int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packed, const float* b7,
                    const float* mid_snake_alpha_exp, const float* mid_snake_inv_beta,
@@ -108,6 +115,10 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
                     const float* up_filter, const float* down_filter, float* y,
                     int B, int C, int T, void* stream);
 
+/* bc_tanh_fwd: nn.Tanh (vq/codec_decoder.py:80) called on its own (decoder.model used as the
+ * reference's nn.Sequential); the fused decoder runs it in the last conv's epilogue (epilogue = 1). */
+int bc_tanh_fwd(const float* x, float* y, long long n, void* stream);
+
 /* ---- ResLSTM ----------------------------------------------------------------------------------------
  * Replaces ResLSTM.forward (vq/module.py:156-167): rearrange b f t -> b t f, nn.LSTM(H, H,
  * num_layers, batch_first=True) (unidirectional), + skip, rearrange back.  x, out: [B][H][T].
@@ -117,10 +128,16 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
  * pointer arrays are HOST arrays of device pointers.  out = snake(y + x) when out_snake_alpha_exp !=
  * NULL (the Activation1d that follows the ResLSTM in both stacks), else y + x.  workspace:
  * bc_lstm_workspace_floats(B, H, T) device floats.  H % 16 == 0.
- * mode 1 with H in {256, 512, 1024, 1536}: the recurrence runs as ONE persistent launch per layer
- * (H/8 co-resident workgroups, W_hh register-resident, 3xbf16-split MFMA); otherwise one launch per
- * step (fp32 MFMA).  bc_lstm_status(reset) returns how many persistent-launch workgroups gave up
- * waiting for a neighbour (bounded spin; 0 in every correct run), synchronising the device. */
+ * Modes 1 and 3 with H in {256, 512, 1024, 1536}: the recurrence runs as ONE persistent launch per
+ * layer (H/8 workgroups that must all be resident at once — checked against the kernel's occupancy,
+ * else 3 — W_hh register-resident; mode 1 3xbf16-split, mode 3 2xfp16-split MFMA); otherwise one
+ * launch per step (fp32 MFMA).
+ * TIMEOUT STATUS: the call zeroes ((int*)workspace)[0] on the stream, and every persistent
+ * workgroup that gives up waiting for a neighbour (bounded spin; never in a correct run) adds 1 to it
+ * and leaves, so `out` is then WRONG.  The caller must read that int after the call completes and
+ * treat nonzero as an error before consuming `out` (the Python package raises BigCodecLibraryError).
+ * bc_lstm_status(reset) returns the same count summed over the process's calls (diagnostic),
+ * synchronising the device. */
 long long bc_lstm_hh_packed_floats(int H, int mode);
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode);
 long long bc_lstm_workspace_floats(int B, int H, int T);

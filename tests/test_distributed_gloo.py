@@ -3,6 +3,7 @@ block partition + per-batch all-gather of the index tensor."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -43,20 +44,127 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_all_gather(world):
+def _run(target, world, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + extra) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=120) for _ in range(world))
+    try:
+        results = dict(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
+    return results
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_all_gather(world):
+    results = _run(_worker, world)
     for r in range(world):
         got = results[r]
         assert sorted(got) == list(range(10))
         for cid, row in got.items():
             assert row == [cid * 100 + f for f in range(5)]
+
+
+N_CLIPS, BATCH, NQ, NF = 11, 3, 2, 4
+
+
+def _fake_source(clip0, n):
+    """(n, 1, T) whose sample 0 carries the global clip id (the fake model reads it back)."""
+    x = torch.zeros((n, 1, 8))
+    x[:, 0, 0] = torch.arange(clip0, clip0 + n, dtype=torch.float32)
+    return x
+
+
+def _fake_codes(ids):
+    ids = torch.as_tensor(ids, dtype=torch.int64)
+    return ids[None, :, None] * 100 + torch.arange(NQ)[:, None, None] * 10 + torch.arange(NF)[None, None, :]
+
+
+def _extract_worker(rank, world, port, q, fail_rank, fail_batch):
+    """extract_sharded itself (the product function) with a fake model that raises on one rank's batch."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audiotokenization_amd.extract import extract_sharded
+
+    calls = {"n": 0}
+
+    def model(x):
+        bi = calls["n"]
+        calls["n"] += 1
+        if rank == fail_rank and bi == fail_batch:
+            raise RuntimeError("injected failure")
+        return {"indices": _fake_codes(x[:, 0, 0].long())}
+
+    sunk = {}
+    st = extract_sharded(model, N_CLIPS, 8, BATCH, rank=rank, world=world, device=torch.device("cpu"),
+                         sink=lambda cid, arr: sunk.__setitem__(cid, arr.copy()), source=_fake_source)
+    q.put((rank, (st, sunk)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,fail_batch", [(2, 1, 0), (3, 0, 0), (3, 2, 1)])
+def test_extract_sharded_survives_a_failed_batch(world, fail_rank, fail_batch):
+    """a rank whose batch raises must still join the batch's collectives, so the
+    job finishes; the failure is counted (extract_indices.py:565-574) and every other clip arrives."""
+    from audiotokenization_amd.extract import shard_range
+
+    results = _run(_extract_worker, world, fail_rank, fail_batch)
+    flo, fhi = shard_range(N_CLIPS, fail_rank, world)
+    lost = list(range(flo + fail_batch * BATCH, min(flo + (fail_batch + 1) * BATCH, fhi)))
+    assert lost, "the injected batch must hold real clips"
+    for r in range(world):
+        st, sunk = results[r]
+        lo, hi = shard_range(N_CLIPS, r, world)
+        assert st.errors == (len(lost) if r == fail_rank else 0)
+        assert st.error_items == (lost if r == fail_rank else [])
+        assert st.clips == hi - lo - st.errors
+        assert st.job_errors == len(lost) and st.job_clips == N_CLIPS - len(lost)
+        if r == 0:
+            assert sorted(sunk) == [c for c in range(N_CLIPS) if c not in lost]
+            for cid, arr in sunk.items():
+                assert arr.dtype == np.int16 and arr.shape == (NF, NQ)
+                np.testing.assert_array_equal(arr, _fake_codes([cid])[:, 0, :].T.numpy())
+        else:
+            assert sunk == {}
+
+
+def _all_fail_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audiotokenization_amd.extract import extract_sharded
+
+    def model(x):
+        raise RuntimeError("every batch fails")
+
+    st = extract_sharded(model, 5, 8, 2, rank=rank, world=world, device=torch.device("cpu"), sink=lambda *a: None,
+                         source=_fake_source)
+    q.put((rank, st))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_extract_sharded_all_ranks_fail():
+    results = _run(_all_fail_worker, 2)
+    for r, st in results.items():
+        assert st.clips == 0 and st.job_errors == 5 and st.job_clips == 0
+
+
+def test_extract_sharded_single_process_no_dist():
+    """world = 1 without an initialised process group: same bookkeeping, no collective."""
+    from audiotokenization_amd.extract import extract_sharded
+
+    sunk = {}
+    st = extract_sharded(lambda x: _fake_codes(x[:, 0, 0].long()), 7, 8, 3, device=torch.device("cpu"),
+                         sink=lambda cid, arr: sunk.__setitem__(cid, arr), source=_fake_source)
+    assert st.clips == 7 and st.errors == 0 and st.batches == 3 and sorted(sunk) == list(range(7))

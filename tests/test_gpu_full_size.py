@@ -1,0 +1,139 @@
+"""Full-size parity at BASELINE.json's headline configs against the REFERENCE's own outputs
+(tools/make_golden_full.py, SURVEY §8(c) golden items 2-3; reference anchor extract_indices.py:510-532).
+
+  config 2: 64 x 240 000-sample clips (clips 0..63), `default` model, encode + VQ -> all 76 800 indices
+            equal to the reference's, except at frames whose fp64 top-2 distance gap is below 1e-6
+            (GAP_TOL; the fixture's smallest gap over all 76 800 frames is 2.2e-6, so any flip fails);
+            latent of clip 0 within 1e-4 (max|d| / max|ref|); 16 fp64 random-projection fingerprints of
+            every clip's latent within 1e-5 x sum|latent|.
+  config 3: the same clips decoded from our post-VQ embedding -> waveforms of clips 0-1 within MSE <= 1e-12
+            and max|d| <= 1e-5 of the reference's; sum(y^2), sum(y) and 16 projections of every clip within
+            1e-6 relative of their scale (equal codes make this the decoder's error alone).
+  30 s:     one 720 000-sample clip (T = 3600 LSTM steps, config 5's length) in the fp32-class precisions:
+            3600 indices (gap tol 1e-6), the latent's last 64 frames within 1e-4, latent fingerprints.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import GAP_TOL, assert_close_rel, build_models, index_mismatches
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def projections(shape, n=16, seed=20261016):
+    """tools/make_golden_full.py:projections (same seed -> the same +-1 vectors)."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 2, size=(n,) + tuple(shape)).astype(np.float64) * 2.0 - 1.0
+
+
+def check_fingerprints(got: np.ndarray, want_fp: np.ndarray, proj: np.ndarray, tol: float, what: str):
+    """|<got, r_k> - want_k| <= tol * sum|got| for every projection r_k (per clip)."""
+    g = np.asarray(got, dtype=np.float64).reshape(-1)
+    fp = proj.reshape(proj.shape[0], -1) @ g
+    scale = np.abs(g).sum()
+    err = float(np.abs(fp - want_fp).max() / scale)
+    assert err <= tol, f"{what}: fingerprint error {err:.2e} > {tol:.0e}"
+    return err
+
+
+@pytest.fixture(scope="module")
+def default_model(dev):
+    return build_models("default", device=dev)
+
+
+@pytest.mark.parametrize("precision", ["h3", "x6"])
+def test_config2_all_76800_indices_vs_reference(dev, golden, default_model, precision):
+    from audiotokenization_amd import _lib
+    from audiotokenization_amd.extract import synth_batch
+
+    g = golden("full_config2_default.npz")
+    meta = g["meta"]
+    B, T = meta["n_clips"], meta["n_samples"]
+    enc, dec, *_ = default_model
+    old = _lib.precision_mode()
+    try:
+        _lib.set_precision(precision)
+        with torch.no_grad():
+            x = synth_batch(B, T, 0, dev)  # clips 0..63 = bench.py's rank-0 batch
+            lat = enc(x)
+            codes = dec(lat, vq=True)[1]
+            torch.cuda.synchronize()
+    finally:
+        _lib._mode = old
+    assert codes.shape == (1, B, T // 200)
+    got = codes[0].cpu().numpy()
+    n_bad, worst = index_mismatches(got, g["codes"].astype(np.int64), g["gap"], gap_tol=GAP_TOL)
+    print(f"config 2 [{precision}]: {n_bad} / {got.size} index mismatches vs the reference, worst certified gap "
+          f"{worst:.2e} (tol {GAP_TOL:.0e}); smallest gap in the fixture {float(g['gap'].min()):.2e}")
+    lat_np = lat.cpu().numpy()
+    assert_close_rel(lat_np[0], g["latent0"], 1e-4, "latent clip 0")
+    proj = projections(lat_np.shape[1:])
+    worst_fp = max(check_fingerprints(lat_np[i], g["latent_fp"][i], proj, 1e-5, f"latent clip {i}") for i in range(B))
+    print(f"config 2 [{precision}]: latent fingerprints of {B} clips, worst relative error {worst_fp:.2e}")
+
+
+def test_config3_waveforms_vs_reference(dev, golden, default_model):
+    """Full round trip at config 3's size: our encoder -> VQ -> decoder vs the reference's waveforms."""
+    from audiotokenization_amd.extract import synth_batch
+
+    g2 = golden("full_config2_default.npz")
+    g3 = golden("full_config3_default.npz")
+    B, T = g3["meta"]["n_clips"], g3["meta"]["n_samples"]
+    enc, dec, *_ = default_model
+    with torch.no_grad():
+        x = synth_batch(B, T, 0, dev)
+        post, codes, _ = dec(enc(x), vq=True)
+        del x
+        wav = dec(post, vq=False)
+        torch.cuda.synchronize()
+    assert wav.shape == (B, 1, T)
+    same = (codes[0].cpu().numpy() == g2["codes"]).all(axis=1)  # a flipped code changes its clip's waveform
+    w = wav[:, 0].cpu().double().numpy()
+    for i in range(2):
+        if same[i]:
+            d = w[i] - g3["wav01"][i].astype(np.float64)
+            mse, mx = float((d * d).mean()), float(np.abs(d).max())
+            print(f"config 3 clip {i}: waveform mse {mse:.2e} max {mx:.2e}")
+            assert mse <= 1e-12 and mx <= 1e-5
+    proj = projections((T,))
+    worst = 0.0
+    for i in np.nonzero(same)[0]:
+        sq = float((w[i] * w[i]).sum())
+        assert abs(sq - g3["sumsq"][i]) <= 1e-6 * g3["sumsq"][i], (i, sq, g3["sumsq"][i])
+        assert abs(float(w[i].sum()) - g3["sum"][i]) <= 1e-6 * np.abs(w[i]).sum()
+        worst = max(worst, check_fingerprints(w[i], g3["wav_fp"][i], proj, 1e-6, f"waveform clip {i}"))
+    print(f"config 3: {int(same.sum())} / {B} clips with identical codes checked, worst fingerprint error {worst:.2e}")
+    assert same.sum() >= B - 2
+
+
+@pytest.mark.parametrize("precision", ["h3", "x6"])
+def test_30s_clip_lstm_3600_steps_vs_reference(dev, golden, default_model, precision):
+    """Config 5's clip length in fp32-class arithmetic: the persistent ResLSTM runs 3600 steps."""
+    from audiotokenization_amd import _lib
+    from audiotokenization_amd.extract import synth_batch
+
+    g = golden("long30_default.npz")
+    meta = g["meta"]
+    enc, dec, *_ = default_model
+    old = _lib.precision_mode()
+    try:
+        _lib.set_precision(precision)
+        with torch.no_grad():
+            lat = enc(synth_batch(1, meta["n_samples"], meta["clip0"], dev))
+            codes = dec(lat, vq=True)[1]
+            torch.cuda.synchronize()
+    finally:
+        _lib._mode = old
+    assert codes.shape == (1, 1, 3600)
+    n_bad, worst = index_mismatches(codes[0].cpu().numpy(), g["codes"][None].astype(np.int64), g["gap"][None],
+                                    gap_tol=GAP_TOL)
+    print(f"30 s clip [{precision}]: {n_bad} / 3600 index mismatches, worst certified gap {worst:.2e}")
+    lat_np = lat[0].cpu().numpy()
+    assert_close_rel(lat_np[:, -64:], g["latent_tail"], 1e-4, "latent last 64 frames")
+    err = check_fingerprints(lat_np, g["latent_fp"], projections(lat_np.shape), 1e-5, "latent 30 s")
+    print(f"30 s clip [{precision}]: latent fingerprint error {err:.2e}")

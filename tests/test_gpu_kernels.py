@@ -453,3 +453,31 @@ def test_abi_rejects_bad_args(dev):
     assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 99, None) == 1
     assert lib.bc_conv1d_fwd(1, 1, None, None, None, None, 1, None, 1, 48, 10, 48, 10, 7, 1, 1, 3, 0, 5109, None) == 1
     assert lib.bc_vq_argmin(1, 1, 1, 1, 10, 8192, 4, None) == 3
+
+
+def test_lstm_timeout_is_loud(dev):
+    """a persistent ResLSTM launch whose workgroups give up waiting (forced here with
+    a poll limit of 1 through the diagnostic bc_debug_set_lstm_spin_limit) must raise, not return wrong
+    latents; the next normal call is correct again."""
+    import ctypes
+
+    from audiotokenization_amd import synth
+    from helpers import build_models
+
+    lib = L.load()
+    setter = lib.bc_debug_set_lstm_spin_limit
+    setter.argtypes = [ctypes.c_longlong]
+    setter.restype = ctypes.c_int
+    enc, dec, *_ = build_models("base", device=dev)
+    x = torch.from_numpy(synth.synth_clips(2, 24000, clip0=0)).unsqueeze(1).to(dev)
+    with torch.no_grad():
+        good = enc(x)
+        assert setter(1) == 0
+        try:
+            with pytest.raises(L.BigCodecLibraryError, match="timed out"):
+                enc(x)
+        finally:
+            assert setter(0) == 0
+        again = enc(x)
+        torch.cuda.synchronize()
+    assert torch.equal(good, again)

@@ -3,7 +3,7 @@ size-independent properties at BASELINE.json's full sizes.
 
 Tolerances (fp32 throughout, north_star "reconstructed waveforms within a stated fp32 tolerance"):
   latent (encoder output)      max|d| / max|ref| <= 1e-4
-  VQ indices                   equal, except frames whose fp64 top-2 distance gap < 1e-4
+  VQ indices                   equal, except frames whose fp64 top-2 distance gap < 1e-6 (helpers.GAP_TOL)
                                (reported; a near-tie flips under any fp32 reassociation —
                                SURVEY.md §0 item 7: two valid CPU builds already differ)
   waveform (decoding the reference's own z_q)   MSE <= 1e-12 and max|d| <= 1e-5
@@ -170,3 +170,40 @@ def test_full_size_clip_against_oracle(dev, prec):
     gap = top2_gap(ze_ref, torch.from_numpy(dsd["quantizer.layers.0._codebook.weight"]))
     n_bad, worst = index_mismatches(codes.cpu().numpy(), codes_ref.numpy(), gap)
     print(f"10 s default clip [{prec}]: {n_bad} / 1200 index mismatches, worst certified gap {worst:.2e}")
+
+
+@pytest.mark.parametrize("nq", [2, 4])
+def test_rvq_multi_quantizer_against_reference(dev, golden, nq):
+    """vq_num_quantizers > 1 against the REFERENCE's ResidualVQ (tests/golden/rvq_base_nq*.npz,
+    residual_vq.py:21-40): the reference latent through our RVQ on the GPU -> codes (Nq, B, F) equal,
+    except at a frame certified at its first differing layer (the fixture's per-layer fp64 top-2 gap <
+    GAP_TOL; later layers then see another residual); post-VQ within 1e-5; vq2emb within 1e-6.  Then
+    the whole base encoder + RVQ from the synthetic clip."""
+    from audiotokenization_amd import synth
+    from helpers import GAP_TOL
+
+    g = golden(f"rvq_base_nq{nq}.npz")
+    meta = g["meta"]
+    enc, dec, *_ = build_models("base", device=dev, vq_num_quantizers=nq)
+    with torch.no_grad():
+        post, codes, loss = dec(torch.from_numpy(g["latent"]).to(dev), vq=True)
+        x = torch.from_numpy(synth.synth_clips(meta["n_clips"], meta["n_samples"], clip0=meta["clip0"])).unsqueeze(1)
+        codes_e2e = dec(enc(x.to(dev)), vq=True)[1]
+        emb = dec.vq2emb(torch.from_numpy(g["codes"]).permute(1, 2, 0).contiguous().to(dev))
+        torch.cuda.synchronize()
+    assert tuple(codes.shape) == g["codes"].shape and float(loss.abs().sum()) == 0.0
+    for name, c in (("latent-fed", codes), ("end to end", codes_e2e)):
+        gi, wi = c.cpu().numpy().reshape(nq, -1), g["codes"].reshape(nq, -1)
+        gap = g["gap"].reshape(nq, -1)
+        bad = np.nonzero((gi != wi).any(0))[0]
+        for f in bad:
+            first = int(np.nonzero(gi[:, f] != wi[:, f])[0][0])
+            assert gap[first, f] < GAP_TOL, f"{name}: frame {f} layer {first} flipped at gap {gap[first, f]:.2e}"
+        print(f"rvq nq={nq} [{name}]: {bad.size} / {gi.shape[1]} frames differ")
+        if name == "latent-fed":
+            ok = np.ones(gi.shape[1], bool)
+            ok[bad] = False
+            gq = post.cpu().permute(0, 2, 1).reshape(-1, post.shape[1])[ok]
+            wq = torch.from_numpy(g["post"]).permute(0, 2, 1).reshape(-1, post.shape[1])[ok]
+            assert_close_rel(gq, wq, 1e-5, f"rvq nq={nq} post")
+    assert_close_rel(emb.cpu(), torch.from_numpy(g["vq2emb"]), 1e-6, f"rvq nq={nq} vq2emb")

@@ -5,7 +5,7 @@
 set -u
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timer}
+ARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timer --no-x6}
 PASSES=${PMC_PASSES:-"FETCH_SIZE WRITE_SIZE MFMA"}
 for pass in $PASSES; do
   ctr=$pass

@@ -1,4 +1,5 @@
 # Ablation of the one-launch ResidualUnit (BC_RU_DEBUG bits, timing only): profiles/r01g_ru_ablation.txt
+# needs a library built with BIGCODEC_ABLATION=1 (python audiotokenization_amd/build_lib.py): the product build compiles the switches out
 set -u
 mkdir -p gpurun_out
 for dbg in 0 1 2 4 8 3 15; do

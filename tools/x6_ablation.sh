@@ -1,4 +1,5 @@
 # Ablation of the conv kernel main loop (BC_X6_DEBUG bits: 1 no A copies, 2 no B loads, 4 no B stores, 8 no epilogue);
+# needs a library built with BIGCODEC_ABLATION=1 (python audiotokenization_amd/build_lib.py): the product build compiles the switches out
 # results in profiles/r01f_h3_x6kernel_ablation.txt.  Timing only: the outputs are wrong with any bit set.
 set -u
 mkdir -p gpurun_out
