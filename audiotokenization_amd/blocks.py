@@ -22,6 +22,7 @@ import torch.nn as nn
 from torch.nn import Parameter
 
 from . import _lib as L
+from . import ops
 from .conv import WNConv1d, WNConvTranspose1d
 from .modules import Activation1d, SnakeBeta, _DeviceCache, _as_input, _cpu, _pkey
 
@@ -125,19 +126,12 @@ class ResidualUnit(nn.Module):
             raise ValueError("ResidualUnit: raw and activated inputs differ in shape")
         sa, sb = next_act.act.coeffs(dev) if next_act is not None else (None, None)
         dual = next_act is not None and want_raw
-        y = torch.empty_like(x_raw)
-        y2 = torch.empty_like(x_raw) if dual else None
         tm = L.active_timer()
         ev = tm.begin() if tm is not None else None
-        if lazy:
-            s1a, s1b = self.first_act.act.coeffs(dev)
-            L.call("bc_resunit_fwd_snake_in", x_raw.data_ptr(), s1a.data_ptr(), s1b.data_ptr(), w7.data_ptr(),
-                   L.ptr(b7), s2a.data_ptr(), s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb),
-                   y.data_ptr(), L.ptr(y2), B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_raw))
-        else:
-            L.call("bc_resunit_fwd", x_raw.data_ptr(), x_act.data_ptr(), w7.data_ptr(), L.ptr(b7),
-                   s2a.data_ptr(), s2b.data_ptr(), w1.data_ptr(), L.ptr(b1), L.ptr(sa), L.ptr(sb), y.data_ptr(),
-                   L.ptr(y2), B, C, T, conv7.dilation, conv7.pad_left(), cfg, L.stream_of(x_raw))
+        s1a, s1b = self.first_act.act.coeffs(dev) if lazy else (None, None)
+        out = ops.load().resunit(x_raw, None if lazy else x_act, s1a, s1b, w7, b7, s2a, s2b, w1, b1, sa, sb,
+                                 conv7.dilation, conv7.pad_left(), cfg, dual)
+        y, y2 = out[0], (out[1] if dual else None)
         if tm is not None:
             flops = 2.0 * B * C * C * T * 8  # k=7 and k=1
             nbytes = 4.0 * x_raw.numel() * ((2 if lazy else 3) + dual)
@@ -298,30 +292,22 @@ class ResLSTM(nn.Module):
         self.lstm = LSTM(dimension, dimension if not bidirectional else dimension // 2, num_layers,
                          batch_first=True, bidirectional=bidirectional)
 
-    def run(self, x, out_snake=None, state=None):
-        """state (streaming): None, or ((h0, c0) or None, (hT, cT)) with [num_layers][H][B] device buffers;
-        the final (h, c) of this call is written to (hT, cT) (nn.LSTM's (h_n, c_n), unit-major)."""
+    def run(self, x, out_snake=None, state=None, return_state: bool = False):
+        """y = LSTM(x^T)^T + x (then the next Snake when out_snake = (alpha_exp, inv_beta)).  Streaming:
+        state = (h0, c0) [num_layers][H][B] device tensors or None (zeros); with return_state the call
+        returns (y, (h_n, c_n)) in the same layout (nn.LSTM's final state, unit-major)."""
         x = _as_input(x)
         B, H, T = x.shape
-        _, (pwih, pbias, pwhh) = self.lstm.prepared(x.device)
-        lib = L.load()
-        ws = torch.empty(L.checked_size(lib.bc_lstm_workspace_floats(B, H, T), "bc_lstm_workspace_floats"),
-                         device=x.device, dtype=torch.float32)
-        y = torch.empty_like(x)
+        (wih, whh, bias), _ = self.lstm.prepared(x.device)
         sa, sb = out_snake if out_snake is not None else (None, None)
-        if state is None:
-            L.call("bc_reslstm_fwd", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias, pwhh,
-                   L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.stream_of(x))
-        else:
-            init, (hT, cT) = state
-            h0, c0 = init if init is not None else (None, None)
-            L.call("bc_reslstm_fwd_state", x.data_ptr(), y.data_ptr(), B, H, T, self.lstm.num_layers, pwih, pbias,
-                   pwhh, L.ptr(sa), L.ptr(sb), ws.data_ptr(), L.precision_mode(), L.ptr(h0), L.ptr(c0),
-                   hT.data_ptr(), cT.data_ptr(), L.stream_of(x))
-        # include/bigcodec.h: ((int*)workspace)[0] counts persistent workgroups that timed out; the
+        h0, c0 = state if state is not None else (None, None)
+        out = ops.load().reslstm(x, wih, bias, whh, sa, sb, L.precision_mode(), h0, c0, return_state)
+        # include/bigcodec.h: out[1] = the call's count of persistent workgroups that timed out; the
         # codec's forward checks it (L.check_status) before its output can be consumed
-        L.defer_status(ws[:1].view(torch.int32).clone(), f"ResLSTM(H={H}, layers={self.lstm.num_layers}, T={T})")
-        return y
+        L.defer_status(out[1], f"ResLSTM(H={H}, layers={self.lstm.num_layers}, T={T})")
+        if return_state:
+            return out[0], (out[2], out[3])
+        return out[0]
 
     def flow(self, x_raw, want_raw=True, next_act=None) -> Flow:
         if next_act is None:

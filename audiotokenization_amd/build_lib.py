@@ -1,7 +1,9 @@
-"""Build libbigcodec_hip.so (gfx950) in-tree with hipcc.
+"""Build libbigcodec_hip.so (gfx950) in-tree with hipcc, and libbigcodec_ops.so (the torch.ops.bigcodec.*
+custom operators over its C ABI) with g++ against the installed PyTorch-ROCm headers.
 
 The shared library is the product: every compute kernel of the BigCodec path lives in
-audiotokenization_amd/csrc/*.hip and is exported through the C ABI in include/bigcodec.h.
+audiotokenization_amd/csrc/*.hip and is exported through the C ABI in include/bigcodec.h;
+csrc/torch_ops.cpp registers that ABI with the PyTorch dispatcher (TORCH_LIBRARY(bigcodec)).
 Built objects stay in-tree (git-ignored) so they travel with the repo snapshot to the GPU box.
 """
 from __future__ import annotations
@@ -18,6 +20,8 @@ REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD = os.path.join(PKG_DIR, "_build")
 LIB = os.path.join(PKG_DIR, "libbigcodec_hip.so")
+OPS_LIB = os.path.join(PKG_DIR, "libbigcodec_ops.so")
+OPS_SRC = "torch_ops.cpp"
 ARCH = os.environ.get("BIGCODEC_ARCH", "gfx950")
 
 SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip", "conv1d_x6_p3.hip", "resunit_x6.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip",
@@ -71,7 +75,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8, 16)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-soname,libbigcodec_hip.so", *objs, "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stderr}")
@@ -81,5 +85,48 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def _ops_flags():
+    import torch
+    import torch.utils.cpp_extension as ce
+
+    inc = [f"-I{p}" for p in ce.include_paths(device_type="cuda")] + ["-I", os.path.join(REPO, "include")]
+    libs = [f"-L{p}" for p in ce.library_paths(device_type="cuda")]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return (["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+             f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=bigcodec_ops"] + inc,
+            libs + ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", f"-L{PKG_DIR}", "-lbigcodec_hip",
+                    "-Wl,-rpath,$ORIGIN"], torch.__version__)
+
+
+def build_ops(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/torch_ops.cpp (if it, the header or torch changed) into libbigcodec_ops.so."""
+    build(verbose=verbose)
+    cflags, ldflags, tv = _ops_flags()
+    h = hashlib.sha256()
+    for f in (os.path.join(CSRC, OPS_SRC), os.path.join(REPO, "include", "bigcodec.h")):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update((" ".join(cflags + ldflags) + tv).encode())
+    dig = h.hexdigest()
+    stamp = os.path.join(BUILD, "ops_stamp")
+    if not force and os.path.exists(OPS_LIB) and os.path.exists(stamp):
+        with open(stamp) as fh:
+            if fh.read().strip() == dig:
+                return OPS_LIB
+    cxx = os.environ.get("CXX", "g++")
+    tmp = OPS_LIB + ".tmp"
+    cmd = [cxx, *cflags, os.path.join(CSRC, OPS_SRC), "-o", tmp, *ldflags]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"{cxx} failed for {OPS_SRC}:\n{res.stderr}")
+    os.replace(tmp, OPS_LIB)
+    with open(stamp, "w") as fh:
+        fh.write(dig)
+    return OPS_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_ops(force="--force" in sys.argv, verbose=True))

@@ -15,6 +15,7 @@ import torch.nn as nn
 from torch.nn import Parameter
 
 from . import _lib as L
+from . import ops
 from .modules import _DeviceCache, _as_input, _cpu, _pkey
 
 __all__ = ["Conv1dWN", "CausalConv1d", "WNConv1d", "ConvTranspose1dWN", "CausalConvTranspose1d",
@@ -135,18 +136,16 @@ class Conv1dWN(_WNParams, nn.Module):
         Tout = self.out_len(T, pad_left)
         if Tout <= 0:
             raise ValueError(f"input length {T} too short for this convolution")
-        y = torch.empty((B, self.out_channels, Tout), device=x.device, dtype=torch.float32)
-        y2 = torch.empty_like(y) if dual else None
         if residual is not None:
             residual = _as_input(residual)
-            if residual.shape != y.shape:
-                raise ValueError(f"residual shape {tuple(residual.shape)} != output {tuple(y.shape)}")
+            if tuple(residual.shape) != (B, self.out_channels, Tout):
+                raise ValueError(f"residual shape {tuple(residual.shape)} != output {(B, self.out_channels, Tout)}")
         sa, sb = _epilogue_args(out_snake, dual)
         tm = L.active_timer()
         ev = tm.begin() if tm is not None else None
-        L.call("bc_conv1d_fwd", x.data_ptr(), wp.data_ptr(), L.ptr(bias), L.ptr(residual), L.ptr(sa), L.ptr(sb),
-               y.data_ptr(), L.ptr(y2), B, Cin, T, self.out_channels, Tout, self.kernel_size, self.stride,
-               self.dilation, pl, epilogue, cfg, L.stream_of(x))
+        out = ops.load().conv1d(x, wp, bias, residual, sa, sb, self.out_channels, Tout, self.kernel_size, self.stride,
+                                self.dilation, pl, epilogue, cfg, dual)
+        y, y2 = out[0], (out[1] if dual else None)
         if tm is not None:
             flops = 2.0 * B * self.out_channels * Cin * self.kernel_size * Tout
             nbytes = 4.0 * (x.numel() + y.numel() * (1 + (residual is not None) + dual))
@@ -242,15 +241,14 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
         B, Cin, T = x.shape
         if Cin != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
-        _, parr, bias, cfg = self.prepared(x.device)
+        phases, _, bias, cfg = self.prepared(x.device)
         Tout = self.out_len(T)
-        y = torch.empty((B, self.out_channels, Tout), device=x.device, dtype=torch.float32)
-        y2 = torch.empty_like(y) if dual else None
+        if Tout <= 0:
+            raise ValueError(f"input length {T} too short for this transposed convolution")
         sa, sb = _epilogue_args(out_snake, dual)
-        L.call("bc_convT1d_fwd", x.data_ptr(), parr, L.ptr(bias), L.ptr(sa), L.ptr(sb), y.data_ptr(), L.ptr(y2),
-               B, Cin, T, self.out_channels, Tout, self.kernel_size, self.stride, self.padding, cfg,
-               L.stream_of(x))
-        return (y, y2) if dual else y
+        out = ops.load().conv_transpose1d(x, phases, bias, sa, sb, self.out_channels, Tout, self.kernel_size,
+                                          self.stride, self.padding, cfg, dual)
+        return (out[0], out[1]) if dual else out[0]
 
     def forward(self, x):
         return self.run(x)

@@ -261,7 +261,7 @@ std::vector<Tensor> vq(const Tensor& z, const Tensor& w_in, const Tensor& b_in, 
   Tensor post = want_post ? at::empty_like(z) : Tensor();
   ok(bc_vq_fwd(z.data_ptr<float>(), req(z, w_in, "w_in"), req(z, b_in, "b_in"), req(z, cb, "codebook"),
                req(z, cbn, "codebook_norm"), req(z, cbsq, "codebook_sq"), req(z, w_out, "w_out"), req(z, b_out, "b_out"),
-               idx.data_ptr<int64_t>(), want_ze ? ze.data_ptr<float>() : nullptr,
+               reinterpret_cast<long long*>(idx.data_ptr<int64_t>()), want_ze ? ze.data_ptr<float>() : nullptr,
                want_post ? post.data_ptr<float>() : nullptr, i32(B, "B"), i32(D, "D"), i32(T, "T"),
                i32(cb.size(0), "n_codes"), i32(dim, "dim"), stream_of(z)),
      "bc_vq_fwd");
@@ -275,7 +275,7 @@ Tensor vq_argmin(const Tensor& ze, const Tensor& cbn, const Tensor& cbsq) {
   dev(ze, "z_e");
   TORCH_CHECK_VALUE(ze.dim() == 2 && cbn.dim() == 2 && ze.size(1) == cbn.size(1), "bigcodec::vq_argmin: z_e (N, dim), codebook (n, dim)");
   auto idx = at::empty({ze.size(0)}, ze.options().dtype(at::kLong));
-  ok(bc_vq_argmin(ze.data_ptr<float>(), req(ze, cbn, "codebook_norm"), req(ze, cbsq, "codebook_sq"), idx.data_ptr<int64_t>(),
+  ok(bc_vq_argmin(ze.data_ptr<float>(), req(ze, cbn, "codebook_norm"), req(ze, cbsq, "codebook_sq"), reinterpret_cast<long long*>(idx.data_ptr<int64_t>()),
                   ze.size(0), i32(cbn.size(0), "n_codes"), i32(cbn.size(1), "dim"), stream_of(ze)),
      "bc_vq_argmin");
   return idx;
@@ -290,7 +290,7 @@ void vq2emb_launch(const Tensor& idx, int64_t column, const Tensor& cb, const op
   const int64_t nq = idx.size(-1), N = idx.numel() / nq;
   const int64_t D = w_out.has_value() ? w_out->size(0) : cb.size(1);
   TORCH_CHECK_VALUE(out.numel() == N * D, "bigcodec::vq2emb: output size");
-  ok(bc_vq2emb(idx.data_ptr<int64_t>() + column, nq, req(idx, cb, "codebook"), optf(idx, w_out, "w_out"),
+  ok(bc_vq2emb(reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()) + column, nq, req(idx, cb, "codebook"), optf(idx, w_out, "w_out"),
                optf(idx, b_out, "b_out"), out.data_ptr<float>(), N, i32(D, "D"), i32(cb.size(0), "n_codes"),
                i32(cb.size(1), "dim"), accumulate ? 1 : 0, stream_of(idx)),
      "bc_vq2emb");
@@ -326,7 +326,7 @@ Tensor vq2emb_ct(const Tensor& idx, const Tensor& cbs, const Tensor& w_out, cons
   const int64_t B = idx.size(0), T = idx.size(1), nq = idx.size(2), D = w_out.size(1);
   TORCH_CHECK_VALUE(nq <= cbs.size(0), "bigcodec::vq2emb_ct: more index columns than quantizers");
   auto out = at::empty({B, D, T}, idx.options().dtype(at::kFloat));
-  ok(bc_vq2emb_ct(idx.data_ptr<int64_t>(), i32(nq, "nq"), req(idx, cbs, "codebooks"), req(idx, w_out, "w_out"),
+  ok(bc_vq2emb_ct(reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()), i32(nq, "nq"), req(idx, cbs, "codebooks"), req(idx, w_out, "w_out"),
                   req(idx, b_out, "b_out"), out.data_ptr<float>(), i32(B, "B"), i32(T, "T"), i32(D, "D"),
                   i32(cbs.size(1), "n_codes"), i32(cbs.size(2), "dim"), stream_of(idx)),
      "bc_vq2emb_ct");

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import ops
 
 
 def indices_to_numpy(indices: torch.Tensor) -> np.ndarray:
@@ -108,7 +109,9 @@ def batches(lo: int, hi: int, batch: int) -> List[Tuple[int, int]]:
 def synth_batch(n_clips: int, n_samples: int, clip0: int, device) -> torch.Tensor:
     """White-noise clips (B, 1, T) generated in HBM by bc_synth_clips (same values as synth.synth_clips)."""
     x = torch.empty((n_clips, 1, n_samples), device=device, dtype=torch.float32)
-    L.call("bc_synth_clips", x.data_ptr(), n_clips, n_samples, clip0, L.stream_of(x))
+    if not x.is_cuda:
+        raise L.BigCodecLibraryError("synth_batch generates clips on a HIP device")
+    ops.load().synth_clips_(x, clip0)
     return x
 
 

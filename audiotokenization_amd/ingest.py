@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import ops
 
 
 def read_wav(path: str) -> Tuple[np.ndarray, int]:
@@ -128,14 +129,9 @@ class Resampler:
         if not x.is_cuda or x.dtype != torch.float32:
             raise L.BigCodecLibraryError("Resampler takes float32 device tensors")
         x = x.contiguous()
-        lead, n = tuple(x.shape[:-1]), int(x.shape[-1])
-        rows = int(np.prod(lead)) if lead else 1
-        lout = self.out_len(n)
+        lout = self.out_len(int(x.shape[-1]))
         pitch = max(lout, pad_to)
-        y = (torch.zeros if pitch > lout else torch.empty)(lead + (pitch,), device=x.device, dtype=torch.float32)
-        L.call("bc_resample_sinc", x.data_ptr(), y.data_ptr(), self.kern.data_ptr(), rows, n, lout, pitch, self.orig,
-               self.new, self.taps, self.width, L.stream_of(x))
-        return y
+        return ops.load().resample_sinc(x, self.kern, lout, pitch, self.orig, self.new, self.taps, self.width)
 
 
 def load_item(path: str, target_sample_rate: Optional[int] = None, duration: Optional[float] = None,

@@ -21,6 +21,7 @@ import torch.nn as nn
 from torch.nn import Parameter
 
 from . import _lib as L
+from .ops import load as _ops  # torch.ops.bigcodec namespace (loads libbigcodec_ops.so once)
 
 __all__ = [
     "SnakeBeta", "Snake", "Activation1d", "UpSample1d", "DownSample1d", "LowPassFilter1d",
@@ -116,11 +117,7 @@ class SnakeBeta(nn.Module):
     def forward(self, x):
         x = _as_input(x)
         a, ib = self.coeffs(x.device)
-        y = torch.empty_like(x)
-        B, C, T = x.shape
-        L.call("bc_snake_fwd", x.data_ptr(), a.data_ptr(), ib.data_ptr(), y.data_ptr(), B, C, T,
-               L.stream_of(x))
-        return y
+        return _ops().snake(x, a, ib)
 
 
 class Snake(SnakeBeta):
@@ -260,11 +257,7 @@ class Activation1d(nn.Module):
         x = _as_input(x)
         a, ib = self.act.coeffs(x.device)
         fu, fd = self.filters(x.device)
-        y = torch.empty_like(x)
-        B, C, T = x.shape
-        L.call("bc_aa_snake_fwd", x.data_ptr(), a.data_ptr(), ib.data_ptr(), fu.data_ptr(),
-               fd.data_ptr(), y.data_ptr(), B, C, T, L.stream_of(x))
-        return y
+        return _ops().aa_snake(x, a, ib, fu, fd)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -329,13 +322,8 @@ class FactorizedVectorQuantize(nn.Module):
         cbw = self._codebook.weight
 
         def build():
-            lib = L.load()
             cb = _cpu(cbw).contiguous().to(device)
-            cbn = torch.empty_like(cb)
-            csq = torch.empty(cb.shape[0], device=device, dtype=torch.float32)
-            stream = torch.cuda.current_stream(device).cuda_stream
-            L.check(lib.bc_vq_prepare_codebook(cb.data_ptr(), cbn.data_ptr(), csq.data_ptr(), cb.shape[0],
-                                               self.codebook_dim, stream), "bc_vq_prepare_codebook")
+            cbn, csq = _ops().vq_prepare_codebook(cb)
             w_in = self.in_proj.folded_weight().contiguous().to(device)
             b_in = _cpu(self.in_proj.bias).contiguous().to(device)
             w_out = self.out_proj.folded_weight().contiguous().to(device)
@@ -344,13 +332,11 @@ class FactorizedVectorQuantize(nn.Module):
         key = _pkey(cbw, *self.in_proj._params(), *self.out_proj._params()) + (str(device),)
         return self._cache.get(key, build)
 
-    def quantize_into(self, z, idx_out, post_out=None, ze_out=None):
-        """Run the fused kernel; idx_out (B,T) int64 view, post_out (B,D,T) or None."""
-        B, D, T = z.shape
+    def quantize(self, z, want_post: bool = True, want_ze: bool = False):
+        """One fused launch (torch.ops.bigcodec.vq): [indices (B, T) int64, z_e (B, 8, T) if want_ze,
+        post-VQ out_proj(z_q) (B, D, T) if want_post]."""
         cb, cbn, csq, w_in, b_in, w_out, b_out = self.prepared(z.device)
-        L.call("bc_vq_fwd", z.data_ptr(), w_in.data_ptr(), b_in.data_ptr(), cb.data_ptr(), cbn.data_ptr(),
-               csq.data_ptr(), w_out.data_ptr(), b_out.data_ptr(), idx_out.data_ptr(), L.ptr(ze_out),
-               L.ptr(post_out), B, D, T, self.codebook_size, self.codebook_dim, L.stream_of(z))
+        return _ops().vq(z, w_in, b_in, cb, cbn, csq, w_out, b_out, want_ze, want_post)
 
     def forward(self, z):
         if self.training and torch.is_grad_enabled():
@@ -360,9 +346,7 @@ class FactorizedVectorQuantize(nn.Module):
         B, D, T = z.shape
         if D != self.dim:
             raise ValueError(f"expected {self.dim} channels, got {D}")
-        idx = torch.empty((B, T), device=z.device, dtype=torch.int64)
-        post = torch.empty_like(z)
-        self.quantize_into(z, idx, post)
+        idx, post = self.quantize(z)
         commit_loss = _zeros(B, z.device)  # eval: torch.zeros(B) (factorized_vector_quantize.py:66)
         return post, idx, commit_loss
 
@@ -397,26 +381,21 @@ class ResidualVQ(nn.Module):
                                      for size in codebook_size])
         self.num_quantizers = num_quantizers
 
-    def quantize(self, x, idx_out=None, with_post=True):
-        """Fused forward; idx_out optional preallocated (Nq, B, T) int64."""
+    def quantize(self, x, with_post=True):
+        """Fused forward -> (post-VQ sum (B, D, T) or None, indices (Nq, B, T) int64)."""
         x = _as_input(x)
-        B, D, T = x.shape
         nq = len(self.layers)
-        if idx_out is None:
-            idx_out = torch.empty((nq, B, T), device=x.device, dtype=torch.int64)
         if nq == 1:
-            post = torch.empty_like(x) if with_post else None
-            self.layers[0].quantize_into(x, idx_out[0], post)
-            return post, idx_out
+            res = self.layers[0].quantize(x, want_post=with_post)
+            return (res[1] if with_post else None), res[0].unsqueeze(0)
         residual = x.clone()
         out = torch.empty_like(x)
-        q = torch.empty_like(x)
-        stream = L.stream_of(x)
+        idx = []
         for i, layer in enumerate(self.layers):
-            layer.quantize_into(residual, idx_out[i], q)
-            L.call("bc_rvq_update", residual.data_ptr(), out.data_ptr(), q.data_ptr(), residual.numel(),
-                   int(i == 0), stream)
-        return out, idx_out
+            ind, q = layer.quantize(residual)
+            idx.append(ind)
+            _ops().rvq_update_(residual, out, q, i == 0)  # residual -= q; out (+)= q (residual_vq.py:31-33)
+        return out, torch.stack(idx)
 
     def forward(self, x):
         if self.training and torch.is_grad_enabled():
@@ -466,11 +445,7 @@ class ResidualVQ(nn.Module):
         if not 1 <= nq <= len(self.layers):
             raise ValueError(f"{nq} quantizer columns for a {len(self.layers)}-quantizer ResidualVQ")
         cb, w, bb = self.prepared_stack(vq.device)
-        D = w.shape[1]
-        out = torch.empty((B, D, T), device=vq.device, dtype=torch.float32)
-        L.call("bc_vq2emb_ct", vq.data_ptr(), nq, cb.data_ptr(), w.data_ptr(), bb.data_ptr(), out.data_ptr(),
-               B, T, D, cb.shape[1], cb.shape[2], L.stream_of(vq))
-        return out
+        return _ops().vq2emb_ct(vq, cb, w, bb)
 
 
 def _vq2emb_into_strided(self, vq, i, nq, out, proj, accumulate):
@@ -478,14 +453,12 @@ def _vq2emb_into_strided(self, vq, i, nq, out, proj, accumulate):
     if not vq.is_cuda or vq.dtype != torch.int64 or not vq.is_contiguous():
         raise ValueError("vq2emb expects a contiguous int64 device tensor")
     cb, _, _, _, _, w_out, b_out = self.prepared(vq.device)
-    D = self.dim if proj else self.codebook_dim
-    shape = tuple(vq.shape[:-1])
-    N = int(np.prod(shape))
-    if out is None:
-        out = torch.empty(shape + (D,), device=vq.device, dtype=torch.float32)
-    base = vq.data_ptr() + i * vq.element_size()
-    L.call("bc_vq2emb", base, nq, cb.data_ptr(), L.ptr(w_out if proj else None), L.ptr(b_out if proj else None),
-           out.data_ptr(), N, D, self.codebook_size, self.codebook_dim, int(accumulate), L.stream_of(out))
+    if vq.shape[-1] != nq:
+        raise ValueError(f"index tensor has {vq.shape[-1]} columns, expected {nq}")
+    w, b = (w_out, b_out) if proj else (None, None)
+    if out is None or not accumulate:
+        return _ops().vq2emb(vq, i, cb, w, b)
+    _ops().vq2emb_add_(out, vq, i, cb, w, b)
     return out
 
 
@@ -549,8 +522,5 @@ class FSQ(nn.Module):
         if D != self.dim:
             raise ValueError(f"expected dimension of {self.dim} but found dimension of {D}")
         w_in, b_in, w_out, b_out, consts = self.prepared(z.device)
-        idx = torch.empty((B, T), device=z.device, dtype=torch.int32)
-        post = torch.empty_like(z)
-        L.call("bc_fsq_fwd", z.data_ptr(), w_in.data_ptr(), b_in.data_ptr(), w_out.data_ptr(), b_out.data_ptr(),
-               consts.data_ptr(), idx.data_ptr(), post.data_ptr(), B, D, T, self.codebook_dim, L.stream_of(z))
+        post, idx = _ops().fsq(z, w_in, b_in, w_out, b_out, consts)
         return post, idx

@@ -61,11 +61,8 @@ class StreamingEncoder:
         return c.run(xin, residual, pad_left=0)
 
     def _lstm_run(self, m: ResLSTM, h):
-        B, H, _ = h.shape
-        L = m.lstm.num_layers
-        out = (torch.empty((L, H, B), device=h.device), torch.empty((L, H, B), device=h.device))
-        y = m.run(h, state=(self._lstm.get(id(m)), out))
-        self._lstm[id(m)] = out
+        y, state = m.run(h, state=self._lstm.get(id(m)), return_state=True)
+        self._lstm[id(m)] = state
         return y
 
     def push(self, x) -> torch.Tensor:

@@ -198,3 +198,46 @@ def test_h3_pack_layout_and_scaled_split(Cout, Cin, K):
         ws = float(w[row, ci, tap]) * S[row]
         assert h0 == float(np.float16(ws))
         assert abs(ws - h0 - h1) <= abs(ws) * 2.0 ** -22 + 2.0 ** -25
+
+
+def test_torch_ops_registered_with_schemas_and_fakes():
+    """torch.ops.bigcodec.* (csrc/torch_ops.cpp + ops.py): every op is registered, its schema names the
+    ABI arguments, mutating ops mark their outputs (a!), and the fake kernels give the right shapes
+    on meta tensors (no GPU needed)."""
+    import torch
+
+    from audiotokenization_amd import ops
+
+    ns = ops.load()
+    for name in ops.OPS:
+        op = getattr(ns, name)
+        schema = str(op.default._schema)
+        assert schema.startswith(f"bigcodec::{name}("), schema
+        if name.endswith("_"):
+            assert "(a!)" in schema, schema
+    m = lambda *s, dt=torch.float32: torch.empty(*s, device="meta", dtype=dt)  # noqa: E731
+    w = m(10)
+    assert [t.shape for t in ns.conv1d(m(2, 48, 1000), w, None, None, m(96), m(96), 96, 500, 4, 2, 1, 1, 0, 5, True)] \
+        == [(2, 96, 500)] * 2
+    assert ns.conv_transpose1d(m(2, 96, 10), [w, w], None, None, None, 48, 20, 4, 2, 1, 5, False)[0].shape == (2, 48, 20)
+    assert [t.shape for t in ns.resunit(m(2, 48, 64), None, m(48), m(48), w, None, m(48), m(48), w, None, None, None,
+                                        1, 3, 300, False)] == [(2, 48, 64)]
+    assert ns.snake(m(2, 8, 5), m(8), m(8)).shape == (2, 8, 5)
+    assert ns.tanh(m(3, 1, 7)).shape == (3, 1, 7)
+    y, st, hT, cT = ns.reslstm(m(4, 512, 30), [w, w], [w, w], [w, w], None, None, 3, None, None, True)
+    assert y.shape == (4, 512, 30) and st.dtype == torch.int32 and hT.shape == cT.shape == (2, 512, 4)
+    idx, ze, post = ns.vq(m(2, 1024, 12), w, w, m(8192, 8), m(8192, 8), m(8192), w, w, True, True)
+    assert idx.shape == (2, 12) and idx.dtype == torch.int64 and ze.shape == (2, 8, 12) and post.shape == (2, 1024, 12)
+    assert ns.vq2emb(m(2, 12, 3, dt=torch.int64), 1, m(8192, 8), m(1024, 8), m(1024)).shape == (2, 12, 1024)
+    assert ns.vq2emb_ct(m(2, 12, 3, dt=torch.int64), m(3, 8192, 8), m(3, 1024, 8), m(3, 1024)).shape == (2, 1024, 12)
+    post, idx = ns.fsq(m(2, 512, 9), w, w, w, w, w)
+    assert post.shape == (2, 512, 9) and idx.dtype == torch.int32
+    assert ns.resample_sinc(m(3, 160), w, 240, 256, 2, 3, 16, 6).shape == (3, 256)
+
+
+def test_torch_ops_library_links_the_abi_library():
+    """libbigcodec_ops.so calls the C ABI of libbigcodec_hip.so (one instance, found next to it)."""
+    from audiotokenization_amd import ops
+
+    out = subprocess.run(["readelf", "-d", ops.OPS_PATH], capture_output=True, text=True).stdout
+    assert "libbigcodec_hip.so" in out and "$ORIGIN" in out
