@@ -358,6 +358,16 @@ int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int 
   return ctb_to_btc_add_launch(y, skip, nullptr, nullptr, out, B, C, T, S(stream));
 }
 
+int bc_conv1d_kernel_name(int cfg, int K, int stride, int dilation, char* buf, int buflen) {
+  if (!buf || buflen <= 0) return -1;
+  return conv_kernel_name(cfg, K, stride, dilation, buf, buflen);
+}
+
+int bc_resunit_kernel_name(int cfg, int C, int dilation, char* buf, int buflen) {
+  if (!buf || buflen <= 0) return -1;
+  return resunit_kernel_name(cfg, C, dilation, buf, buflen);
+}
+
 int bc_tanh_fwd(const float* x, float* y, long long n, void* stream) {
   if (!x || !y || n < 0) return BC_ERR_ARG;
   return tanh_launch(x, y, n, S(stream));

@@ -39,6 +39,10 @@ bool x6_cfg_valid(int cfg);
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg);
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg);
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st);
+int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n);
+int conv_kernel_name(int cfg_id, int K, int s, int d, char* buf, int n);
+int resunit_kernel_name(int cfg, int C, int d, char* buf, int n);
+int resunit_rr_kernel_name(int C, char* buf, int n);
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id);
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id);
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
@@ -48,6 +52,12 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
                    const float* isa = nullptr, const float* isb = nullptr);
+
+bool resunit_rr_ok(int C, int d);
+int resunit_rr_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
+                      const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb, float* y,
+                      float* y2, int B, int C, int T, int d, int pl, hipStream_t st, const float* isa,
+                      const float* isb);
 
 int snake_launch(const float* x, const float* sa, const float* sb, float* y, int B, int C,
                  long long T, hipStream_t st);

@@ -26,6 +26,8 @@
 //                ds_read_b32 half-wave hit disjoint banks.
 // ConvTranspose1d runs as `stride` polyphase convolutions whose outputs are written with output
 // stride `s` (bc_convT1d_fwd in abi.hip).
+#include <cstdio>
+
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
@@ -297,6 +299,13 @@ static int launch_tile(ConvArgs& a, int B, hipStream_t st) {
   case T * 4 + 1: return launch_tile<MT, WM, NT, WN, 16>(a, B, st);   \
   case T * 4 + 2: return launch_tile<MT, WM, NT, WN, 8>(a, B, st);    \
   case T * 4 + 3: return launch_tile<MT, WM, NT, WN, 4>(a, B, st);
+
+int conv_kernel_name(int cfg_id, int K, int s, int d, char* buf, int n) {
+  if (x6_cfg_valid(cfg_id)) return x6_kernel_name(cfg_id, K, s, d, buf, n);
+  if (!conv_cfg_valid(cfg_id)) return -1;
+  const Tile& t = kTiles[cfg_id / 4];
+  return snprintf(buf, n, "conv1d_mfma_kernel<%d, %d, %d, %d, %d>", t.MT, t.WM, t.NT, t.WN, kBKC[cfg_id % 4]);
+}
 
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st) {
   a.vec = conv_epilogue_vec_ok(a);

@@ -22,6 +22,7 @@
 //                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
 //                at tap 0 and land while the current chunk's taps compute.
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -293,6 +294,19 @@ void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int 
     float* inv = reinterpret_cast<float*>(out + o);
     for (size_t row = 0; row < rsc.size(); ++row) inv[row] = 1.f / rsc[row];
   }
+}
+
+int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n) {
+  if (!x6_cfg_valid(cfg)) return -1;
+  if (const int ps = cfg_phase(cfg)) {  // the stride-1 conv over the phases (x6_launch)
+    K = (K + ps - 1) / ps;
+    s = d = 1;
+  }
+  const X6Tile& t = cfg_tile(cfg);
+  const int P = cfg_planes(cfg);
+  const X6Variant v = x6_variant(t, P, K, s, d);
+  return snprintf(buf, n, "conv1d_x6_kernel<%d, %d, %d, %d, %d, %s, %d>", t.MT, t.NT, t.WM, t.WN, P,
+                  v.pw ? "true" : "false", v.tps);
 }
 
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {

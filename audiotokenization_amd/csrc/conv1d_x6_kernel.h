@@ -381,6 +381,21 @@ inline bool x6_pw_on() {
   return v;
 }
 
+// Which kernel variant a launch of tile t runs (shared by launch_x6 and bc_conv1d_kernel_name, so the
+// name the roofline reports is the one that ran): the pointwise two-chunk-prefetch path (K = 1), two taps
+// per K-step (h3 / bf16 multi-tap launches whose doubled A buffers fit), or one tap per K-step.
+struct X6Variant {
+  bool pw;
+  int tps;
+};
+inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
+  const int ncol = x6_ncol(t, K, s, d);
+  const size_t lds2 = x6_lds(t, ncol, P, s, 2);
+  if (K == 1 && ncol == x6_BN(t) && x6_pw_on()) return {true, 1};
+  if (P <= 2 && K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (t.NT > 1 && lds2 <= 160 * 1024))) return {false, 2};
+  return {false, 1};
+}
+
 template <int MT, int NT, int WM, int WN, int P>
 static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
@@ -404,9 +419,10 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   const size_t lds = x6_lds(t, ncol, P, a.s);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   const size_t lds2 = x6_lds(t, ncol, P, a.s, 2);
-  if (a.K == 1 && ncol == BN && x6_pw_on())
+  const X6Variant v = x6_variant(t, P, a.K, a.s, a.d);
+  if (v.pw)
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
-  else if (P <= 2 && a.K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (NT > 1 && lds2 <= 160 * 1024)))
+  else if (v.tps == 2)
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, (P <= 2 ? 2 : 1)>), dim3(a.nwg), dim3(512),
                        lds2, st, a);
   else

@@ -1,0 +1,447 @@
+// A whole ResidualUnit (vq/module.py:74-89) in one launch for the narrow stages (C <= 96,
+// h3 arithmetic), with the k=7 weights held by the waves instead of the LDS:
+//   y = x + conv1( snake2( conv7_d( snake1(x) ) ) )   (+ the usual epilogue: bias, next Snake, dual)
+//
+// Why a second ResidualUnit kernel (resunit_x6.hip is the general one): at C = 48 / 96 the unit has only
+// 3 / 6 m-tiles, and the 8-wave tile of resunit_x6 makes every wave read every weight fragment from
+// LDS (8 LDS reads per 9 MFMAs at C = 48: LDS-issue bound, 0.13 of the h3 ceiling).
+// Here a workgroup has ONE wave per 16-channel m-tile (C / 16 waves) and each wave computes its
+// m-tile over the whole column tile (NT n-tiles), so
+//   * a weight fragment is used by the waves of one m-tile only: it is streamed from L2 straight into
+//     registers one k=7 tap ahead (no LDS copy, no barrier per K-step; the weights are L2-resident);
+//   * the LDS holds only the input tile (2 fp16 planes) and then the activated k=7 output h: every
+//     B-fragment read feeds 3 MFMAs, per wave 2 reads per 3 MFMAs per n-tile with no A reads at all;
+//   * the 16 channels past the last full 32-channel chunk (C = 48) run on v_mfma_f32_16x16x16_f16
+//     instead of a zero-padded 16x16x32 (the unit's k=7 and k=1 MFMA work at C = 48 drops by 1/4).
+// One workgroup per column tile (a persistent variant kept loop-invariant staging geometry live and
+// spilled).  Phases (barriers only inside the workgroup): stage x (snake on load, h3 block
+// scale per 32-channel chunk, split, LDS) -> phase 1 k=7 -> bridge (h = snake2(acc + b7), tile
+// block scale, split, LDS over the dead input tile) -> phase 2 k=1 from LDS with register weights ->
+// conv_epilogue (residual x, bias, next Snake, dual output).
+// Weights use resunit_x6's packing for the unit's cfg (bc_conv1d_pack, one m-group of C rows).
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "bc_common.h"
+#include "bc_internal.h"
+#include "conv_epilogue.h"
+#include "x6_common.h"
+
+namespace bc {
+
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int RR_MAX_DIL = 9;  // input tile sized for the k=7 halo at dilation <= 9 (BigCodec: 1, 3, 9)
+
+struct RRArgs {
+  const float* x;              // staged input: x_act, or x_raw with snake on load
+  const unsigned char* w7;     // packed k=7 planes [chunk][tap][plane][m-tile][lane][8 fp16]
+  const unsigned char* w1;     // packed k=1 planes [chunk][plane][m-tile][lane][8 fp16]
+  const float* b7;             // k=7 bias or nullptr
+  const float* w7sc;           // 1 / k=7 row scale (h3 packing)
+  const float* s2a;            // Snake between the convs: alpha_exp, inv_beta [C]
+  const float* s2b;
+  const float* isa;            // snake on load (first Activation1d) or nullptr
+  const float* isb;
+  long long xbs;               // floats per clip of x
+  int T, d, pl, ncol, ntn, ntiles;
+};
+
+// input tile, full chunk c, plane p: [ncol][64 B] (16-B channel groups XOR-swizzled by (col >> 1) & 3)
+__device__ __forceinline__ int rr_bfull(int col, int g) { return col * 64 + 16 * (g ^ ((col >> 1) & 3)); }
+// 16-channel tail, plane p: [ncol][32 B], the two 8-channel halves swapped on odd (col >> 3): the
+// ds_read_b64 fragments of 16 consecutive columns hit 64 distinct banks
+__device__ __forceinline__ int rr_btail(int col, int h) { return col * 32 + 16 * (h ^ ((col >> 3) & 1)); }
+// h tile (phase-2 A operand): full chunk [BN][64 B] swizzled by (n >> 2) & 3, tail [BN][32 B]
+__device__ __forceinline__ int rr_hfull(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
+
+// one k=7 tap of a full 32-channel chunk over NT n-tiles: B fragments from the input tile (2 planes at
+// column col0 + 16 j), the h3 products hi*lo, lo*hi, hi*hi with the weights (a0 = hi, a1 = lo plane)
+template <int NT>
+__device__ __forceinline__ void rr_taps(floatx4 (&acc)[NT], const unsigned char* B0, int bpl, int col0, int lg,
+                                        const f16x8_t& a0, const f16x8_t& a1) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = col0 + 16 * j;
+    const f16x8_t b0 = *reinterpret_cast<const f16x8_t*>(B0 + rr_bfull(col, lg));
+    const f16x8_t b1 = *reinterpret_cast<const f16x8_t*>(B0 + bpl + rr_bfull(col, lg));
+    floatx4 v = acc[j];
+    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0, v, 0, 0, 0);
+    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, v, 0, 0, 0);
+    v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, v, 0, 0, 0);
+    acc[j] = v;
+  }
+}
+
+template <int C, int WN>
+struct RRGeom {
+  static constexpr int MQ = C / 16;          // m-tiles; wave w owns m-tile w % MQ, column group w / MQ
+  static constexpr int NW = MQ * WN;         // waves
+  static constexpr int NCF = C / 32;         // full 32-channel chunks
+  static constexpr bool TAIL = (C % 32) != 0;  // a 16-channel tail chunk
+  static constexpr int NTHR = 64 * NW;
+  static constexpr int NCK = NCF + (TAIL ? 1 : 0);  // packed chunks (the tail is a padded chunk)
+};
+
+// NT n-tiles per wave, WN column groups: BN = 16 * NT * WN columns per tile
+template <int C, int NT, int WN>
+__global__ void __launch_bounds__(64 * (C / 16) * WN, 2) resunit_rr_kernel(RRArgs r, ConvArgs e) {
+  using G = RRGeom<C, WN>;
+  constexpr int MQ = G::MQ, NW = G::NW, NCF = G::NCF, NCK = G::NCK, NTHR = G::NTHR;
+  constexpr bool TAIL = G::TAIL;
+  constexpr int BN = 16 * NT * WN;
+  constexpr int PIECE = 2 * MQ * 1024;                                  // bytes per (chunk, tap) of w7 (2 planes)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_rr[];
+  __shared__ unsigned smax[2][NW];
+  __shared__ unsigned hmax[NW];
+  __shared__ float sisa[C], sisb[C];  // snake-on-load coefficients (the unit's first Activation1d)
+
+  const int ncol = r.ncol;
+  const int bpl = ncol * (64 * NCF + 32 * (TAIL ? 1 : 0));  // bytes per input-tile plane
+  const int tbase = ncol * 64 * NCF;                          // tail offset within a plane
+  constexpr int HPL = BN * (64 * NCF + 32 * (TAIL ? 1 : 0));  // bytes per h-tile plane
+  constexpr int HTB = BN * 64 * NCF;
+  unsigned char* Bs = smem_rr;
+  unsigned char* Hs = smem_rr;  // aliases the input tile once phase 1 is over
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = wave % MQ;                 // this wave's m-tile
+  const int cb = (wave / MQ) * NT * 16;    // and its first column within the tile
+  const int lr = lane & 15, lg = lane >> 4;
+  const bool act_in = r.isa != nullptr;
+  if (act_in)
+    for (int c = tid; c < C; c += NTHR) {
+      sisa[c] = r.isa[c];
+      sisb[c] = r.isb[c];
+    }
+
+  // weight fragments, streamed from L2 into registers (each is read by the waves of one m-tile only):
+  // full chunk c, tap t, plane p: 16x16x32 A operand (row lr, k = 8 lg + i); the tail chunk's 16x16x16 A
+  // operand (k = 4 lg + i) is gathered out of the padded chunk's 16x16x32 packing
+  const unsigned char* w7q = r.w7 + q * 1024 + lane * 16;
+  const unsigned char* w7t = r.w7 + q * 1024 + (lr + 16 * (lg >> 1)) * 16 + 8 * (lg & 1);
+  auto wf = [&](int c, int t, int p) {
+    return *reinterpret_cast<const f16x8_t*>(w7q + (long long)(c * 7 + t) * PIECE + p * MQ * 1024);
+  };
+  auto wt = [&](int t, int p) {
+    return *reinterpret_cast<const f16x4_t*>(w7t + (long long)(NCF * 7 + t) * PIECE + p * MQ * 1024);
+  };
+  const int co4 = q * 16 + 4 * lg;  // the bridge's channels co4 .. co4 + 3 (phase-1 output rows of this lane)
+
+  // one column tile per workgroup; XCD-aware order: neighbouring tiles share an L2 (input halos)
+  const int tile = xcd_remap(blockIdx.x, r.ntiles);
+  {
+    lds_barrier();  // sisa / sisb
+    const int b = tile / r.ntn;
+    const int n0 = (tile - b * r.ntn) * BN;
+    const int in0 = n0 - r.pl;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(r.x + (long long)b * r.xbs), 0, C * r.T * 4, 0x00020000);
+
+    // ---------------- stage the input tile, chunk by chunk (h3 scale: min over the chunks so far) ----------------
+    float xs = 0.f;   // running scale
+    float csc[NCK];   // the scale each chunk was split with
+    auto stage = [&](int c, auto npc, int ch_base, auto store_pair) {
+      constexpr int NP = decltype(npc)::value;           // channel pairs of the chunk (16, or 8 for the tail)
+      constexpr int KP = (NP + NW - 1) / NW;             // pairs per wave
+      constexpr int KC = (BN + 6 * RR_MAX_DIL + 63) / 64;  // 64-column blocks
+      float v0[KP][KC], v1[KP][KC];
+#pragma unroll
+      for (int i = 0; i < KP; ++i) {
+        const int pp = wave + NW * i;
+        const int ch = ch_base + 2 * (pp < NP ? pp : 0);
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int col = lane + 64 * k;
+          const int t = in0 + col;
+          const bool ok = pp < NP && col < ncol && t >= 0 && t < r.T;
+          const unsigned o0 = ok ? (unsigned)((ch * r.T + t) * 4) : 0xfffffff0u;
+          v0[i][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o0, 0, 0));
+          v1[i][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? o0 + (unsigned)r.T * 4 : o0, 0, 0));
+        }
+      }
+      unsigned m = 0;
+#pragma unroll
+      for (int i = 0; i < KP; ++i) {
+        const int pp = wave + NW * i;
+        const int ch = ch_base + 2 * (pp < NP ? pp : 0);
+        const float a0 = act_in ? sisa[ch] : 0.f, b0 = act_in ? sisb[ch] : 0.f;
+        const float a1 = act_in ? sisa[ch + 1] : 0.f, b1 = act_in ? sisb[ch + 1] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          if (act_in) {  // out-of-range samples read 0 and snake(0) = 0: the reference's zero padding
+            v0[i][k] = snake(v0[i][k], a0, b0);
+            v1[i][k] = snake(v1[i][k], a1, b1);
+          }
+          const unsigned u0 = __float_as_uint(fabsf(v0[i][k])), u1 = __float_as_uint(fabsf(v1[i][k]));
+          m = m > u0 ? m : u0;
+          m = m > u1 ? m : u1;
+        }
+      }
+      m = wave_max_u32(m);
+      if (lane == 0) smax[c & 1][wave] = m;
+      lds_barrier();
+      unsigned mm = smax[c & 1][0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) mm = mm > smax[c & 1][w] ? mm : smax[c & 1][w];
+      const float sc = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(mm));
+      xs = (c == 0 || sc < xs) ? sc : xs;
+      csc[c] = xs;
+#pragma unroll
+      for (int i = 0; i < KP; ++i) {
+        const int pp = wave + NW * i;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int col = lane + 64 * k;
+          if (pp < NP && col < ncol) {
+            unsigned h, l;
+            split2_h(v0[i][k] * xs, v1[i][k] * xs, h, l);
+            store_pair(pp, col, h, l);
+          }
+        }
+      }
+    };
+#pragma unroll
+    for (int c = 0; c < NCF; ++c)
+      stage(c, std::integral_constant<int, 16>{}, c * 32, [&](int p, int col, unsigned h, unsigned l) {
+        unsigned char* dst = Bs + c * ncol * 64 + rr_bfull(col, p >> 2) + (p & 3) * 4;
+        *reinterpret_cast<unsigned*>(dst) = h;
+        *reinterpret_cast<unsigned*>(dst + bpl) = l;
+      });
+    if constexpr (TAIL)
+      stage(NCF, std::integral_constant<int, 8>{}, NCF * 32, [&](int p, int col, unsigned h, unsigned l) {
+        unsigned char* dst = Bs + tbase + rr_btail(col, p >> 2) + (p & 3) * 4;
+        *reinterpret_cast<unsigned*>(dst) = h;
+        *reinterpret_cast<unsigned*>(dst + bpl) = l;
+      });
+    lds_barrier();
+
+    // ---------------- phase 1: k=7, this wave's 16 channels x NT n-tiles, weights one tap ahead ----------------
+    floatx4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float cur = csc[0];
+    const int d = r.d;
+    const int col0 = cb + lr;
+#pragma unroll
+    for (int c = 0; c < NCF; ++c) {
+      if (csc[c] < cur) {
+        const float rs = csc[c] / cur;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] *= rs;
+        cur = csc[c];
+      }
+      const unsigned char* B0 = Bs + c * ncol * 64;
+      f16x8_t a0 = wf(c, 0, 0), a1 = wf(c, 0, 1);
+#pragma unroll 1
+      for (int t = 0; t < 7; ++t) {
+        const int tn = t < 6 ? t + 1 : 6;
+        const f16x8_t n0v = wf(c, tn, 0), n1v = wf(c, tn, 1);
+        rr_taps(acc, B0, bpl, col0 + t * d, lg, a0, a1);
+        a0 = n0v;
+        a1 = n1v;
+      }
+    }
+    if constexpr (TAIL) {
+      // the tail accumulates into its own registers: a 16x16x16 MFMA chained straight onto a 16x16x32
+      // accumulator was observed to read it early (intermittently wrong lanes), so the chains never mix
+      floatx4 acct[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acct[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const unsigned char* BT = Bs + tbase;
+      f16x4_t a0 = wt(0, 0), a1 = wt(0, 1);
+#pragma unroll 1
+      for (int t = 0; t < 7; ++t) {
+        const int tn = t < 6 ? t + 1 : 6;
+        const f16x4_t n0v = wt(tn, 0), n1v = wt(tn, 1);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int off = rr_btail(col0 + 16 * j + t * d, lg >> 1) + 8 * (lg & 1);
+          const f16x4_t b0 = *reinterpret_cast<const f16x4_t*>(BT + off);
+          const f16x4_t b1 = *reinterpret_cast<const f16x4_t*>(BT + bpl + off);
+          floatx4 v = acct[j];
+          v = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, b0, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, b1, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, b0, v, 0, 0, 0);
+          acct[j] = v;
+        }
+        a0 = n0v;
+        a1 = n1v;
+      }
+      // scales are powers of two: acc * (tail scale / cur) is exact
+      const float rs = NCF > 0 && csc[NCF] < cur ? csc[NCF] / cur : 1.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = NCF > 0 ? acc[j] * rs + acct[j] : acct[j];
+      cur = csc[NCF];
+    }
+
+    // k=1 weights as the phase-2 B operand (column = output channel lr of m-tile q), fetched now so they
+    // land during the bridge
+    f16x8_t U[NCF][2];
+    f16x4_t UT[2];
+#pragma unroll
+    for (int c = 0; c < NCF; ++c)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        U[c][p] = *reinterpret_cast<const f16x8_t*>(r.w1 + ((c * 2 + p) * MQ + q) * 1024 + lane * 16);
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        UT[p] = *reinterpret_cast<const f16x4_t*>(r.w1 + ((NCF * 2 + p) * MQ + q) * 1024 + (lr + 16 * (lg >> 1)) * 16 +
+                                                  8 * (lg & 1));
+    }
+
+    // ---------------- bridge: h = snake2(acc * (1 / (x scale * w7 row scale)) + b7), tile scale, split ----------------
+    {
+      const float xinv = 1.f / cur;
+      unsigned m = 0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co4 + rr;
+        const float bias = r.b7 ? r.b7[co] : 0.f;
+        const float sc = r.w7sc[co] * xinv, sa = r.s2a[co], sb = r.s2b[co];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const float v = snake(acc[j][rr] * sc + bias, sa, sb);
+          acc[j][rr] = v;
+          const unsigned u = __float_as_uint(fabsf(v));
+          m = m > u ? m : u;
+        }
+      }
+      m = wave_max_u32(m);
+      if (lane == 0) hmax[wave] = m;
+    }
+    lds_barrier();  // every wave is past phase 1: the input tile is dead, Hs may overwrite it
+    float hs;
+    {
+      unsigned mm = hmax[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) mm = mm > hmax[w] ? mm : hmax[w];
+      hs = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(mm));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = col0 + 16 * j;
+      unsigned h0, l0, h1, l1;
+      split2_h(acc[j][0] * hs, acc[j][1] * hs, h0, l0);
+      split2_h(acc[j][2] * hs, acc[j][3] * hs, h1, l1);
+      unsigned char* dst;
+      if (co4 < NCF * 32) {
+        dst = Hs + (co4 / 32) * BN * 64 + rr_hfull(n, (co4 % 32) / 8) + (co4 % 8) * 2;
+      } else {
+        const int ct = co4 - NCF * 32;
+        dst = Hs + HTB + rr_btail(n, ct / 8) + (ct % 8) * 2;
+      }
+      *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){h0, h1};
+      *reinterpret_cast<u32x2_t*>(dst + HPL) = (u32x2_t){l0, l1};
+    }
+    lds_barrier();
+
+    // ---------------- phase 2: k=1 from the h tile (input as the MFMA A operand: transposed output) ----------------
+    floatx4 acc2[1][NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = col0 + 16 * j;
+      floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCF; ++c) {
+        const unsigned char* src = Hs + c * BN * 64 + rr_hfull(n, lg);
+        const f16x8_t h0 = *reinterpret_cast<const f16x8_t*>(src);
+        const f16x8_t h1 = *reinterpret_cast<const f16x8_t*>(src + HPL);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0, U[c][1], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h1, U[c][0], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0, U[c][0], v, 0, 0, 0);
+      }
+      if constexpr (TAIL) {  // own accumulator (see phase 1)
+        const unsigned char* src = Hs + HTB + rr_btail(n, lg >> 1) + 8 * (lg & 1);
+        const f16x4_t h0 = *reinterpret_cast<const f16x4_t*>(src);
+        const f16x4_t h1 = *reinterpret_cast<const f16x4_t*>(src + HPL);
+        floatx4 vt = floatx4{0.f, 0.f, 0.f, 0.f};
+        vt = __builtin_amdgcn_mfma_f32_16x16x16f16(h0, UT[1], vt, 0, 0, 0);
+        vt = __builtin_amdgcn_mfma_f32_16x16x16f16(h1, UT[0], vt, 0, 0, 0);
+        vt = __builtin_amdgcn_mfma_f32_16x16x16f16(h0, UT[0], vt, 0, 0, 0);
+        v = NCF > 0 ? v + vt : vt;
+      }
+      acc2[0][j] = v;
+    }
+    conv_epilogue<1, NT, true>(e, acc2, b, q * 16, n0 + cb, lane, 1.f / hs);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+// BC_RU_RR=0 keeps every unit on resunit_x6 (A/B timing).
+static bool rr_enabled() {
+  static const bool v = [] {
+    const char* s = getenv("BC_RU_RR");
+    return !s || atoi(s) != 0;
+  }();
+  return v;
+}
+
+bool resunit_rr_ok(int C, int d) { return rr_enabled() && C == 48 && d >= 1 && d <= RR_MAX_DIL; }
+
+template <int C, int NT, int WN>
+static int launch_rr(RRArgs& r, ConvArgs& e, int B, hipStream_t st) {
+  using G = RRGeom<C, WN>;
+  constexpr int BN = 16 * NT * WN;
+  r.ncol = BN + 6 * r.d;
+  r.ntn = (r.T + BN - 1) / BN;
+  const long long ntiles = (long long)r.ntn * B;
+  if (ntiles <= 0) return BC_OK;
+  if (ntiles > 0x7fffffffLL || (long long)C * r.T * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  r.ntiles = (int)ntiles;
+  const size_t lds_b = 2 * (size_t)r.ncol * (64 * G::NCF + 32 * (G::TAIL ? 1 : 0));
+  const size_t lds_h = 2 * (size_t)BN * (64 * G::NCF + 32 * (G::TAIL ? 1 : 0));
+  const size_t lds = lds_b > lds_h ? lds_b : lds_h;
+  if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
+  const long long nwg = ntiles;
+  hipLaunchKernelGGL((resunit_rr_kernel<C, NT, WN>), dim3((unsigned)nwg), dim3(G::NTHR), lds, st, r, e);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+int resunit_rr_kernel_name(int C, char* buf, int n) {
+  if (C != 48) return -1;
+  return snprintf(buf, n, "resunit_rr_kernel<48, 4, 1>");  // the launch below
+}
+
+// x_raw / x_act / isa as resunit_launch; w7 / w1 packed for a resunit cfg whose tile has BM = C (one m-group)
+int resunit_rr_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
+                      const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb, float* y,
+                      float* y2, int B, int C, int T, int d, int pl, hipStream_t st, const float* isa,
+                      const float* isb) {
+  if (!resunit_rr_ok(C, d)) return BC_ERR_UNSUPPORTED;
+  const int nck = (C + X6_BKC - 1) / X6_BKC, QA = C / 16;
+  RRArgs r{};
+  r.x = isa ? x_raw : x_act;
+  r.w7 = reinterpret_cast<const unsigned char*>(w7);
+  r.w1 = reinterpret_cast<const unsigned char*>(w1);
+  r.b7 = b7;
+  r.w7sc = reinterpret_cast<const float*>(r.w7 + (long long)nck * 7 * 2 * QA * 1024);
+  r.s2a = s2a;
+  r.s2b = s2b;
+  r.isa = isa;
+  r.isb = isb;
+  r.xbs = (long long)C * T;
+  r.T = T;
+  r.d = d;
+  r.pl = pl;
+  ConvArgs e{};
+  e.bias = b1; e.res = x_raw; e.osa = osa; e.osb = osb; e.y = y; e.y2 = y2;
+  e.ybs = (long long)C * T; e.rbs = e.ybs;
+  e.Cout = C; e.Nout = T; e.yT = T; e.ostride = 1; e.ooff = 0; e.epi = 0;
+  e.wsc = reinterpret_cast<const float*>(r.w1 + (long long)nck * 2 * QA * 1024);
+  e.vec = conv_epilogue_vec_ok(e);
+  // measured (tools/ru_rr_sweep.sh, profiles/r02_ru_rr_sweep.txt): 4 n-tiles per wave, one column group
+  // (BN = 64, 3 waves): 5.25-5.36 ms vs 5.45-5.74 for resunit_x6 at C = 48, T = 240 000, B = 64; every
+  // variant lost at C = 96 (7.1-11 ms vs 6.5), which stays on resunit_x6
+  if (C == 48) return launch_rr<48, 4, 1>(r, e, B, st);
+  return BC_ERR_UNSUPPORTED;
+}
+
+}  // namespace bc

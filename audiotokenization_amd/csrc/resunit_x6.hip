@@ -18,6 +18,7 @@
 // Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
 // P = 3: x6 (3 bf16 planes, 6 products); P = 2: h3 (2 block-scaled fp16 planes, 3 products; the k=7
 // input is scaled per staged chunk as in conv1d_x6.hip, h per workgroup tile from its block maximum).
+#include <cstdio>
 #include <cstdlib>
 
 #include "bc_common.h"
@@ -516,10 +517,24 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
   return BC_OK;
 }
 
+int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
+  const bool h3 = cfg >= 300 && cfg < 400;
+  if (!(h3 || (cfg >= 100 && cfg < 200)) || cfg != resunit_select_cfg(C, d, h3 ? 3 : 1)) return -1;
+  if (h3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, buf, n);
+  const X6Tile& t = x6_tile(cfg);
+  return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, h3 ? 2 : 3,
+                  ru_tps(t, C, d, h3 ? 2 : 3));
+}
+
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
                    const float* isa, const float* isb) {
+  if (cfg >= 300 && cfg < 400 && resunit_rr_ok(C, d)) {  // h3 at C = 48 / 96: the register-weight kernel
+    const int rc = resunit_rr_launch(x_raw, x_act, w7, b7, s2a, s2b, w1, b1, osa, osb, y, y2, B, C, T, d, pl, st,
+                                     isa, isb);
+    if (rc != BC_ERR_UNSUPPORTED) return rc;
+  }
   ConvArgs a{};
   a.x = x_act; a.w = w7; a.bias = b7;
   a.xbs = (long long)C * T;

@@ -64,6 +64,8 @@ def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
     planes = targs[4] if kname.startswith(("conv1d_x6_kernel", "resunit_x6_kernel")) and len(targs) >= 5 else None
+    if kname.startswith("resunit_rr_kernel"):  # resunit_rr.hip: h3 (two fp16 planes) only
+        planes = "2"
     if planes == "1":
         return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"
     if planes == "2":
@@ -90,7 +92,7 @@ def kernel_table(summ, steps, probe, n=8):
         rows.append({"kernel": name, "launches_per_step": d["launches"] // steps,
                      "ms_per_step": round(d["ms_total"] / steps, 3), "tflops": round(tf, 1),
                      "frac_mfma_spec": round(tf / peak, 3),
-                     "frac_mfma_probe": round(tf * mult / probe, 3) if name.startswith(("conv1d_x6", "resunit_x6")) else None,
+                     "frac_mfma_probe": round(tf * mult / probe, 3) if name.startswith(("conv1d_x6", "resunit_")) else None,
                      "gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 3)})
     return rows
 

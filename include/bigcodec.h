@@ -115,6 +115,13 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
                     const float* up_filter, const float* down_filter, float* y,
                     int B, int C, int T, void* stream);
 
+/* Diagnostics (bench.py's roofline attribution, no compute): the kernel symbol a bc_conv1d_fwd launch with
+ * this cfg (K = the conv's kernel size, before any phase decomposition) or a bc_resunit_fwd launch runs, as
+ * rocprofv3 prints it without "void bc::" and the argument list; decided by the launchers' own code.
+ * Returns the name's length (written NUL-terminated, truncated to buflen), or -1 for an invalid cfg. */
+int bc_conv1d_kernel_name(int cfg, int K, int stride, int dilation, char* buf, int buflen);
+int bc_resunit_kernel_name(int cfg, int C, int dilation, char* buf, int buflen);
+
 /* bc_tanh_fwd: nn.Tanh (vq/codec_decoder.py:80) called on its own (decoder.model used as the
  * reference's nn.Sequential); the fused decoder runs it in the last conv's epilogue (epilogue = 1). */
 int bc_tanh_fwd(const float* x, float* y, long long n, void* stream);

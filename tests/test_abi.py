@@ -241,3 +241,28 @@ def test_torch_ops_library_links_the_abi_library():
 
     out = subprocess.run(["readelf", "-d", ops.OPS_PATH], capture_output=True, text=True).stdout
     assert "libbigcodec_hip.so" in out and "$ORIGIN" in out
+
+
+def test_kernel_names_come_from_the_launchers():
+    """bc_conv1d_kernel_name / bc_resunit_kernel_name (the roofline attribution) name the template the
+    launcher instantiates for the selected cfg: the tile's template arguments and the plane count."""
+    lib = L.load()
+    for (Cout, Cin, K, s, d, mode) in [(384, 384, 7, 1, 9, 3), (768, 768, 1, 1, 1, 3), (768, 384, 10, 5, 1, 3),
+                                       (192, 192, 7, 1, 3, 1), (96, 48, 4, 2, 1, 3), (48, 1, 7, 1, 1, 3)]:
+        cfg = lib.bc_conv1d_select_cfg(Cout, Cin, K, s, d, mode)
+        name = L.conv_kernel_name(cfg, K, s, d)
+        base = cfg % 1000
+        if 100 <= base < 400:
+            mt, nt, wm, wn = L.X6_CFGS[base % 100 + 100]
+            planes = {1: 3, 2: 1, 3: 2}[base // 100]
+            assert name.startswith(f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, "), (cfg, name)
+            assert name.endswith(("true, 1>", "false, 1>", "false, 2>")), name
+        else:
+            mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
+            assert name == f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>", name
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1>")  # pointwise
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_rr_kernel<48, 4, 1>"
+    n96 = L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 3), 96, 3)
+    assert n96.startswith("resunit_x6_kernel<") and ", 2, " in n96, n96
+    with pytest.raises(L.BigCodecLibraryError):
+        L.conv_kernel_name(12345, 7)

@@ -246,6 +246,7 @@ def test_h3_block_scaling(dev, Cin, K, pw):
 
 
 @pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, False, 1, 700), (96, 3, False, 2, 513),
+                                           (48, 3, False, 1, 24000), (48, 1, False, 3, 4096), (48, 9, True, 2, 777),
                                            (64, 9, False, 2, 300), (16, 3, True, 2, 257), (64, 1, False, 1, 260),
                                            (96, 9, True, 1, 999), (32, 1, False, 3, 64)])
 @pytest.mark.parametrize("ru_prec", ["x6", "h3"])

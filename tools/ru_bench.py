@@ -28,6 +28,7 @@ def main():
     p.add_argument("--iters", type=int, default=5)
     p.add_argument("--cfg", type=int, default=-1)
     p.add_argument("--precision", default="h3")
+    p.add_argument("--lazy", action="store_true", help="snake on load (x_act = None), as the encoder flow runs it")
     a = p.parse_args()
     L.set_precision(a.precision)
     dev = torch.device("cuda", 0)
@@ -42,7 +43,7 @@ def main():
     cfg = a.cfg if a.cfg >= 0 else ru._fused_cfg()
 
     def run():
-        return ru._flow_fused(cfg, x_raw, x_act, a.dual, nxt)
+        return ru._flow_fused(cfg, x_raw, None if a.lazy else x_act, a.dual, nxt)
 
     run()
     torch.cuda.synchronize()
@@ -54,9 +55,9 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     fl = 2.0 * a.B * a.C * a.C * a.T * 8
-    nb = 4.0 * x_act.numel() * (3 + a.dual)
+    nb = 4.0 * x_act.numel() * (3 + a.dual - a.lazy)
     print(f"resunit C={a.C} d={a.d} T={a.T} B={a.B} dual={int(a.dual)} cfg={cfg} ({L.resunit_kernel_name(cfg, a.C, a.d)}) "
-          f"dbg={os.environ.get('BC_RU_DEBUG', '0')}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TFLOP/s  {nb / ms / 1e6:.0f} GB/s",
+          f"rr={os.environ.get('BC_RU_RR', '1')} lazy={int(a.lazy)}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TFLOP/s  {nb / ms / 1e6:.0f} GB/s",
           flush=True)
 
 
