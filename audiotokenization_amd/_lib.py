@@ -52,6 +52,8 @@ _SIGS = {
     "bc_ctb_to_btc_add": (I, [P, P, P, I, I, I, P]),
     "bc_synth_clips": (I, [P, I, L, L, P]),
     "bc_tanh_fwd": (I, [P, P, L, P]),
+    "bc_flac_info": (I, [P, L, P, P, P, P]),
+    "bc_flac_decode": (L, [P, L, P, I, L, I]),
     "bc_conv1d_kernel_name": (I, [I, I, I, I, C.c_char_p, I]),
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
 }

@@ -25,7 +25,7 @@ OPS_SRC = "torch_ops.cpp"
 ARCH = os.environ.get("BIGCODEC_ARCH", "gfx950")
 
 SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip", "conv1d_x6_p3.hip", "resunit_x6.hip", "resunit_rr.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip",
-           "vq.hip", "resample.hip", "probe.hip", "abi.hip"]
+           "vq.hip", "resample.hip", "probe.hip", "abi.hip", "flac.cpp"]
 HEADERS = ["bc_common.h", "bc_internal.h", "conv_epilogue.h", "x6_common.h", "conv1d_x6_kernel.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
@@ -63,7 +63,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(BUILD, src.replace(".hip", ".o"))
+        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -247,3 +247,162 @@ def extract_sharded(model, n_clips: int, n_samples: int, batch: int, rank: int =
     """Encode clips [0, n_clips) clip-sharded over `world` ranks (ShardedExtractor.run)."""
     return ShardedExtractor(model, n_clips, n_samples, batch, rank, world, device, gather, sink, group,
                             source).run()
+
+
+# ------------------------------------------------------------------------------------------------
+# the extraction CLI: python -m audiotokenization_amd.extract  (extract_indices.py:375-589)
+# ------------------------------------------------------------------------------------------------
+VALID_SUBSETS = {"dev-clean", "dev-other", "test-clean", "test-other", "train-clean-100", "train-clean-360",
+                 "train-other-500"}
+
+
+def find_items(root: str, subsets, dataset_path: str = "LibriTTS", ext_audio: str = ".flac"):
+    """LibriTTSDataset's walker (extract_indices.py:181-248): per subset, <root>/<dataset_path>/<subset>
+    or else <root>/<subset>, every *<ext_audio> below it (rglob) -> [(subset, subset_path, fileid)]."""
+    from pathlib import Path
+
+    items = []
+    for subset in ([subsets] if isinstance(subsets, str) else subsets):
+        if subset not in VALID_SUBSETS:
+            print(f"Warning: Subset '{subset}' not in standard {dataset_path} list: {VALID_SUBSETS}")
+        subset_path = os.path.join(root, dataset_path, subset)
+        if not os.path.isdir(subset_path):
+            subset_path = os.path.join(root, subset)
+            if not os.path.isdir(subset_path):
+                raise RuntimeError(f"Dataset subset not found at expected locations relative to root '{root}': "
+                                   f"check structure.")
+        for p in sorted(Path(subset_path).rglob(f"*{ext_audio}")):
+            items.append((subset, subset_path, p.stem))
+    return items
+
+
+def item_path(subset_path: str, fileid: str, ext_audio: str) -> str:
+    """load_libritts_item's path (extract_indices.py:48-72): <subset_path>/<speaker>/<chapter>/<fileid><ext>
+    from a LibriTTS (spk_chapter_seg_utt) or LibriSpeech (spk-chapter-utt) file id."""
+    parts = fileid.split("_")
+    if len(parts) != 4:
+        parts = fileid.split("-")
+        if len(parts) < 3:
+            raise ValueError(f"Cannot parse speaker/chapter from fileid: {fileid}")
+    return os.path.join(subset_path, parts[0], parts[1], fileid + ext_audio)
+
+
+def build_lm(save_path: str, device):
+    """extract_indices.py:430-460 + BigCodecModel(ckpt, cfg): hydra/config.yaml and the first existing
+    last.ckpt candidate (config.find_checkpoint) -> a CodecLightningModule on `device`."""
+    from .config import find_checkpoint, load_config
+    from .lightning_shim import CodecLightningModule
+
+    config_path, ckpt_path = find_checkpoint(save_path)
+    if not os.path.exists(config_path):
+        raise FileNotFoundError(f"Config file not found at {config_path}")
+    if ckpt_path is None:
+        raise FileNotFoundError(f"Checkpoint file not found under {save_path}")
+    return CodecLightningModule.from_checkpoint(ckpt_path, load_config(config_path)).to(device).eval()
+
+
+def run_extraction(lm, items, output_dir: str, sample_rate: Optional[int], duration: Optional[float],
+                   ext_audio: str, device, rank: int = 0, world: int = 1, workers: int = 4, log=print):
+    """The extraction loop (extract_indices.py:497-574) for this rank's block of the file list: host decode
+    (FLAC / WAV) of the next files on `workers` threads while the current one runs on the GPU, then
+    resample (GPU) -> encode -> VQ -> (F, Nq) int16 -> <output_dir>/<subset>/<spk>/<chapter>/<fileid>.npy.
+    Per-file failures are counted, not fatal.  Returns (saved, errors) of this rank."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from .ingest import read_audio, load_item
+
+    model = BigCodecModel(lm)
+    lo, hi = shard_range(len(items), rank, world)
+    mine = items[lo:hi]
+    saved = errors = 0
+
+    def read(it):
+        subset, subset_path, fileid = it
+        path = item_path(subset_path, fileid, ext_audio)
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"Audio file not found at: {path}")
+        return read_audio(path)
+
+    workers = max(1, workers)
+    with ThreadPoolExecutor(max_workers=workers) as pool:
+        futs = {j: pool.submit(read, mine[j]) for j in range(min(workers, len(mine)))}
+        for i, (subset, _, fileid) in enumerate(mine):
+            if i + workers < len(mine):  # keep `workers` files decoding ahead of the GPU
+                futs[i + workers] = pool.submit(read, mine[i + workers])
+            try:
+                x, sr = futs.pop(i).result()
+                wav, _ = load_item(None, sample_rate, duration, None, device, decoded=(x, sr))
+                with torch.no_grad():
+                    out = model(wav.unsqueeze(0))
+                indices = out.get("indices") if isinstance(out, dict) else None
+                if indices is None:
+                    log(f"Warning: No indices found for file: {fileid}. Skipping.")
+                    errors += 1
+                    continue
+                save_indices(output_dir, subset, fileid, indices_to_numpy(indices))
+                saved += 1
+            except Exception as e:  # extract_indices.py:565-574: counted, not fatal
+                log(f"Error processing {fileid}: {type(e).__name__}: {e}")
+                errors += 1
+    return saved, errors
+
+
+def main(argv=None):
+    """python -m audiotokenization_amd.extract --save_path RUN --subsets test-clean [...] — the reference
+    CLI's arguments (extract_indices.py:379-389); --workers (host decode threads) is this build's own.
+    Under torchrun every rank extracts its block of the file list (clip-sharded, no collective on the
+    data path; the saved / error counts are summed at the end)."""
+    import argparse
+    import sys
+
+    p = argparse.ArgumentParser(description="BigCodec index extraction on MI355X (extract_indices.py)")
+    p.add_argument("--dataset_root", type=str, default="../../datasets")
+    p.add_argument("--save_path", type=str, required=True, help="run directory with hydra/config.yaml and last.ckpt")
+    p.add_argument("--output_folder", type=str, default="extracted_indices")
+    p.add_argument("--duration", type=float, default=None)
+    p.add_argument("--sample_rate", type=int, default=16000)
+    p.add_argument("--dataset_path", type=str, default="LibriTTS")
+    p.add_argument("--ext_audio", type=str, default=".flac")
+    p.add_argument("--subsets", type=str, nargs="+", required=True)
+    p.add_argument("--workers", type=int, default=4)
+    a = p.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not os.path.isdir(a.save_path):
+        print(f"Error: Model save path does not exist: {a.save_path}")
+        return 1
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    output_dir = os.path.join(a.save_path, a.output_folder)
+    os.makedirs(output_dir, exist_ok=True)
+    lm = build_lm(a.save_path, device)
+    items = find_items(a.dataset_root, a.subsets, a.dataset_path, a.ext_audio)
+    if not items:
+        print("Error: Dataset is empty. Check dataset root, subset names, and file structure.")
+        return 1
+    if rank == 0:
+        print(f"Dataset size: {len(items)} files, {world} rank(s)")
+    saved, errors = run_extraction(lm, items, output_dir, a.sample_rate, a.duration, a.ext_audio, device, rank,
+                                   world, a.workers)
+    if world > 1:
+        t = torch.tensor([saved, errors], device=device, dtype=torch.int64)
+        dist.all_reduce(t)
+        saved, errors = (int(v) for v in t.tolist())
+        dist.destroy_process_group()
+    if rank == 0:
+        print("\nExtraction complete.")
+        print(f"Successfully saved {saved} index files.")
+        if errors:
+            print(f"Encountered {errors} errors.")
+        print(f"Indices saved in: {output_dir}")
+    sys.stdout.flush()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -4,9 +4,9 @@ The reference loads each utterance with soundfile, trims / zero-pads it to `dura
 torchaudio.transforms.Resample and pads it to a stride (extract_indices.py:36-140, load_libritts_item;
 data_module.py:95-98 does the same resampling for training).  Here:
 
-  * WAV decoding runs on the host (`read_wav`: RIFF/WAVE PCM 8/16/24/32-bit and IEEE float, scaled the
-    way soundfile's float32 reads scale them).  FLAC is not decoded: neither soundfile nor a FLAC
-    decoder exists in this image, so FLAC input is rejected loudly.
+  * Decoding runs on the host: `read_wav` (RIFF/WAVE PCM 8/16/24/32-bit and IEEE float) and `read_flac`
+    (the library's from-scratch RFC 9639 decoder, csrc/flac.cpp: the reference's actual input format),
+    both scaled the way soundfile's float32 reads scale them; `read_audio` picks by the file's magic.
   * Resampling runs on the GPU (`bc_resample_sinc`, csrc/resample.hip) with the sinc-Hann filters built
     here exactly as torchaudio builds them (`sinc_resample_kernel`, float64 -> float32).
   * `load_item` restates load_libritts_item's order of operations for offset_mode='start' (the mode
@@ -19,6 +19,9 @@ from __future__ import annotations
 
 import math
 import struct
+from ctypes import byref as ctypes_ref
+from ctypes import c_int as ctypes_int
+from ctypes import c_longlong as ctypes_longlong
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -35,7 +38,7 @@ def read_wav(path: str) -> Tuple[np.ndarray, int]:
     with open(path, "rb") as fh:
         data = fh.read()
     if data[:4] == b"fLaC":
-        raise NotImplementedError(f"{path}: FLAC decoding is not available in this build (no decoder in the image)")
+        return read_flac(path, data)
     if len(data) < 12 or data[:4] != b"RIFF" or data[8:12] != b"WAVE":
         raise ValueError(f"{path}: not a RIFF/WAVE file")
     fmt = pcm = None
@@ -75,6 +78,41 @@ def read_wav(path: str) -> Tuple[np.ndarray, int]:
     else:
         raise NotImplementedError(f"{path}: WAV format tag {tag} with {bits} bits")
     return np.ascontiguousarray(x.reshape(n, channels).T), int(rate)
+
+
+_FLAC_ERR = {1: "bad argument", 2: "not a FLAC stream or corrupt", 3: "unsupported FLAC feature",
+             4: "CRC mismatch", 5: "more samples than STREAMINFO announced"}
+
+
+def read_flac(path: str, data: bytes = None, check_crc: bool = True, as_int: bool = False) -> Tuple[np.ndarray, int]:
+    """(waveform (C, T), sample_rate) of a FLAC file through bc_flac_decode (host decoder in
+    libbigcodec_hip.so): float32 = sample / 2^(bits - 1) as soundfile.SoundFile(path).read(dtype='float32',
+    always_2d=True).T gives it (extract_indices.py:98-106); as_int -> the int32 samples."""
+    if data is None:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    lib = L.load()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    rate, ch, bits, total = (ctypes_int(), ctypes_int(), ctypes_int(), ctypes_longlong())
+    rc = lib.bc_flac_info(buf.ctypes.data, len(data), ctypes_ref(rate), ctypes_ref(ch), ctypes_ref(bits),
+                          ctypes_ref(total))
+    if rc:
+        raise ValueError(f"{path}: {_FLAC_ERR.get(rc, rc)}")
+    cap = int(total.value) if total.value > 0 else max(4096, len(data))
+    while True:
+        out = np.empty((ch.value, cap), dtype=np.int32 if as_int else np.float32)
+        n = lib.bc_flac_decode(buf.ctypes.data, len(data), out.ctypes.data, int(as_int), cap, int(check_crc))
+        if n == -5 and total.value <= 0:  # unknown length: grow and decode again
+            cap *= 4
+            continue
+        if n < 0:
+            raise ValueError(f"{path}: {_FLAC_ERR.get(-n, n)}")
+        return np.ascontiguousarray(out[:, :n]), int(rate.value)
+
+
+def read_audio(path: str) -> Tuple[np.ndarray, int]:
+    """WAV or FLAC by content (soundfile's float32 read for either)."""
+    return read_wav(path)
 
 
 def sinc_resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6,
@@ -135,11 +173,12 @@ class Resampler:
 
 
 def load_item(path: str, target_sample_rate: Optional[int] = None, duration: Optional[float] = None,
-              pad_to_stride: Optional[int] = None, device="cuda") -> Tuple[torch.Tensor, int]:
+              pad_to_stride: Optional[int] = None, device="cuda",
+              decoded: Optional[Tuple[np.ndarray, int]] = None) -> Tuple[torch.Tensor, int]:
     """extract_indices.py:36-140 (offset_mode='start') for one file: (waveform (C, T) on `device`,
     sample rate).  Trim / zero-pad at the end to int(duration * sr) samples, resample on the GPU,
     zero-pad at the end to a multiple of pad_to_stride."""
-    x, sr = read_wav(path)
+    x, sr = decoded if decoded is not None else read_audio(path)
     if duration is not None:
         n = int(duration * sr)
         x = x[:, :n] if x.shape[1] >= n else np.pad(x, ((0, 0), (0, n - x.shape[1])))

@@ -220,6 +220,21 @@ int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float
 int bc_resample_sinc(const float* x, float* y, const float* kern, int B, long long Lin, long long Lout,
                      long long y_pitch, int orig, int new_freq, int taps, int width, void* stream);
 
+/* ---- FLAC decoding (host code, no device memory) -----------------------------------------------
+ * Replaces soundfile's read of the reference's LibriTTS / LibriSpeech .flac utterances
+ * (extract_indices.py:98-106: sf.SoundFile(...).read(dtype='float32', always_2d=True)).  RFC 9639 streams:
+ * all subframe types, Rice / escaped residuals, wasted bits, stereo decorrelations, 4-32 bit samples.
+ * bc_flac_info: STREAMINFO of an in-memory stream (total_samples 0 = unknown); returns 0, 1 (bad argument),
+ *   2 (not FLAC / corrupt), 3 (unsupported).
+ * bc_flac_decode: every frame into out[channel * max_samples + i] (HOST memory), int32 when out_int32 != 0,
+ *   else float32 = sample * 2^-(bits - 1) (libsndfile's normalised float read); check_crc verifies the
+ *   frame-header CRC-8 and frame CRC-16.  Returns samples per channel, or -1 bad argument, -2 corrupt,
+ *   -3 unsupported, -4 CRC mismatch, -5 more than max_samples samples. */
+int bc_flac_info(const unsigned char* data, long long n, int* sample_rate, int* channels, int* bits,
+                 long long* total_samples);
+long long bc_flac_decode(const unsigned char* data, long long n, void* out, int out_int32, long long max_samples,
+                         int check_crc);
+
 /* ---- Layout helpers & synthetic input --------------------------------------------------------
  * bc_btc_to_ctb: x[B][C][T] -> y[C][T][B];  bc_ctb_to_btc_add: out = transpose(y) + skip.
  * bc_synth_clips: x[B][T] white noise, clip i = clip0 + b (SURVEY.md §8(d) spec). */

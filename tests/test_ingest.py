@@ -67,7 +67,7 @@ def test_read_wav_formats(tmp_path):
     x, sr = ingest.read_wav(str(tmp_path / "e.wav"))
     assert sr == 44100 and np.array_equal(x[0], f32)
     (tmp_path / "f.flac").write_bytes(b"fLaC\0\0\0\0")
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):  # FLAC goes to the FLAC decoder (tests/test_flac.py), which rejects this stub
         ingest.read_wav(str(tmp_path / "f.flac"))
 
 
