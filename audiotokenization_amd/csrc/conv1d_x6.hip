@@ -120,7 +120,11 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 //   pointwise, Cout % 192 == 0     -> 114 (192 x 128): C = 192 / 384 / 768, 10-20 % under 101 / 116
 //                                     (the x256 tiles lose 20-30 % here), except Cout >= 2048 with
 //                                     Cout % 256 == 0 (the LSTM input projection) -> 121
-//   stride 2, Cout % 192 == 0 and <= 384 -> 115 (192 x 64, direct strided B tile): -15 %
+//   stride 2, Cout % 192 == 0 and <= 384 -> 115 (192 x 64, direct strided B tile): -15 %; except
+//                                     Cout % 384 == 0 -> phase-decomposed 120: 192 -> 384 -3.5 %
+//   stride >= 3, d = 1, Cout % 192 == 0 -> phase-decomposed 120 (two taps per K-step fit, 121 runs
+//                                     one): the stride-5 downsampling 384 -> 768 / 768 -> 1536 -3 / -7 %
+//                                     vs phase-decomposed 121 (profiles/r02_s2_sweep.txt)
 static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
   if (s == 1 && K == 1) {
@@ -133,7 +137,12 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
     if ((Cout == 768 || (f321 && !f320)) && fits(21)) return 121;
     if (f320 && fits(20)) return 120;
   }
+  auto phase_fits = [&](int tile) {
+    return x6_ncol(kX6Tiles[tile], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS;
+  };
+  if (s == 2 && d == 1 && Cout % 384 == 0 && phase_fits(20)) return 2000 + 120;
   if (s == 2 && d == 1 && Cout % 192 == 0 && Cout <= 384) return 115;
+  if (s >= 3 && s <= 16 && d == 1 && Cout % 192 == 0 && phase_fits(20)) return 1000 * s + 120;
   if (s >= 3 && s <= 16 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[21], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS)
     return 1000 * s + 121;
   if (s >= 3 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[2], K, s, d) <= 32 * X6_MAXCOL_ITERS) return 102;
@@ -305,8 +314,8 @@ int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n) {
   const X6Tile& t = cfg_tile(cfg);
   const int P = cfg_planes(cfg);
   const X6Variant v = x6_variant(t, P, K, s, d);
-  return snprintf(buf, n, "conv1d_x6_kernel<%d, %d, %d, %d, %d, %s, %d>", t.MT, t.NT, t.WM, t.WN, P,
-                  v.pw ? "true" : "false", v.tps);
+  return snprintf(buf, n, "conv1d_x6_kernel<%d, %d, %d, %d, %d, %s, %d, %s>", t.MT, t.NT, t.WM, t.WN, P,
+                  v.pw ? "true" : "false", v.tps, v.db ? "true" : "false");
 }
 
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {

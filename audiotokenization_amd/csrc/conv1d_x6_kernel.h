@@ -39,7 +39,11 @@ namespace bc {
 // PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
 // TPS: taps per K-step of the multi-tap path (1 or 2): one A copy, one wait and one barrier cover
 // TPS (chunk, tap) units, i.e. BK = 32 * TPS per barrier.
-template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1>
+// DB (multi-tap path, kst >= 3 for P == 2, >= 2 otherwise): two B buffers; chunk c + 1 is staged into the
+// idle one during chunk c's K-steps (maxima published at step 1, split and stored at step 2 for h3 /
+// step 1 otherwise) instead of behind an extra barrier at the chunk's last step, so the staging VALU and
+// LDS writes overlap the other waves' MFMAs.
+template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
 // one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
@@ -57,8 +61,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   const bool bswz = bpitch == 64;
   // byte offset of 16-B channel group g (channels 8g..8g+7 of the chunk) of column col
   auto bgrp = [&](int col, int g) { return col * bpitch + 16 * (bswz ? (g ^ ((col >> 1) & 3)) : g); };
-  unsigned char* Bs = smem_x6;                            // [P][ncol][bpitch]
-  unsigned char* As = smem_x6 + P * bplane;               // [2][TPS][P][QA][1 KiB]
+  unsigned char* Bs = smem_x6;                            // [DB ? 2 : 1][P][ncol][bpitch]
+  unsigned char* As = smem_x6 + (DB ? 2 : 1) * P * bplane;  // [2][TPS][P][QA][1 KiB]
+  const unsigned char* Br = Bs;                           // B buffer the K-steps read
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int mt_idx = wg % a.ntm;
@@ -147,7 +152,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
   };
   float xs = 1.f;  // P == 2: scale of the staged chunk and of the accumulator
-  auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI]) {
+  auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI], unsigned char* Bt, float sc) {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
       const int col = bcl + 32 * i;
@@ -155,14 +160,14 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
         const float v0 = w0[i], v1 = w1[i];
         if constexpr (P == 2) {
           unsigned h, m;
-          split2_h(v0 * xs, v1 * xs, h, m);
-          unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
+          split2_h(v0 * sc, v1 * sc, h, m);
+          unsigned char* p = Bt + bgrp(col, bp >> 2) + (bp & 3) * 4;
           *reinterpret_cast<unsigned*>(p) = h;
           *reinterpret_cast<unsigned*>(p + bplane) = m;
           continue;
         }
         const unsigned h = pk_bf16(v0, v1);
-        unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
+        unsigned char* p = Bt + bgrp(col, bp >> 2) + (bp & 3) * 4;
         *reinterpret_cast<unsigned*>(p) = h;
         if (P == 3) {
           const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
@@ -184,8 +189,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
 
   // P == 2, at a chunk boundary (the previous chunk's B tile is no longer read): the next chunk's
   // scale = min(current, its block scale); the accumulator follows exactly (powers of two)
-  auto h3_next_scale = [&](int par) {
-    const float sn = bmax_scale(par);
+  auto rescale_to = [&](float sn) {
     if (sn < xs) {
       const float r = sn / xs;
 #pragma unroll
@@ -195,6 +199,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
       xs = sn;
     }
   };
+  auto h3_next_scale = [&](int par) { rescale_to(bmax_scale(par)); };
 
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
 
@@ -202,48 +207,73 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   auto compute = [&](int buf, int tt, int tap) {
       const unsigned char* Ab = As + buf * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
       // (n-tile j adds 16 * s columns: the swizzle of a stride-1 tile repeats every 8 columns)
-      const unsigned char* Bcol = Bs + bgrp(col_lane + tap * a.d, lane >> 4);
+      const unsigned char* Bcol = Br + bgrp(col_lane + tap * a.d, lane >> 4);
       frag_t bf[NT][P];
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int p = 0; p < P; ++p)
           bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * a.s * bpitch + p * bplane);
+      // A fragments one m-tile ahead (two register sets): m-tile i + 1's reads issue after m-tile i's
+      // first n-tile of MFMAs (pinned by sched barriers), so the lgkmcnt(0) the compiler places before
+      // m-tile i + 1 (pending LDS-DMA makes it count to zero) finds them landed instead of draining
+      // fresh reads before every m-tile
+      // (multi-tap tiles with NT > 1 and at most 24 accumulator tiles: the extra register set spills
+      // in the others)
+      constexpr bool APF = !PW && NT > 1 && MT * NT <= 24;
+      frag_t af[2][P];
+      auto load_a = [&](int i, frag_t (&d)[P]) {
+        const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+#pragma unroll
+        for (int p = 0; p < P; ++p) d[p] = *reinterpret_cast<const frag_t*>(Aq + p * QA * 1024);
+      };
+      load_a(0, af[0]);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
-        const frag_t a0 = *reinterpret_cast<const frag_t*>(Aq);
+        const int sl = APF ? (i & 1) : 0;  // without the prefetch one register set, as before
+        if (!APF && i > 0) load_a(i, af[0]);
+        auto prefetch = [&](int j) {
+          if (APF && j == 1 && i + 1 < MT) {
+            __builtin_amdgcn_sched_barrier(0);
+            load_a(i + 1, af[(i + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        };
+        if (APF) __builtin_amdgcn_sched_barrier(0);  // m-tile i's MFMAs stay after m-tile i - 1's
+        const frag_t a0 = af[sl][0];
         if constexpr (P == 2) {
-          const frag_t a1 = *reinterpret_cast<const frag_t*>(Aq + QA * 1024);
+          const frag_t a1 = af[sl][1];
 #pragma unroll
           for (int j = 0; j < NT; ++j) {
+            prefetch(j);
             floatx4 t = acc[i][j];
             t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][1], a0, t, 0, 0, 0);
             t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a1, t, 0, 0, 0);
             t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a0, t, 0, 0, 0);
             acc[i][j] = t;
           }
-          continue;
+        } else if constexpr (P == 1) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            prefetch(j);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
+          }
         } else {
-        if (P == 1) {
+          const frag_t a1 = af[sl][1];
+          const frag_t a2 = af[sl][P - 1];
 #pragma unroll
-          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
-          continue;
-        }
-        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
-        const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          // operands swapped (input as A): the tile comes out transposed, see conv_epilogue.h
-          floatx4 t = acc[i][j];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
-          acc[i][j] = t;
-        }
+          for (int j = 0; j < NT; ++j) {
+            // operands swapped (input as A): the tile comes out transposed, see conv_epilogue.h
+            prefetch(j);
+            floatx4 t = acc[i][j];
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
+            acc[i][j] = t;
+          }
         }
       }
   };
@@ -256,7 +286,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     lds_barrier();
     xs = bmax_scale(0);
   }
-  store_b(bv0, bv1);
+  store_b(bv0, bv1, Bs, xs);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -273,7 +303,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
         if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
         if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-        if (!BC_ABL(a.dbg, 4)) store_b(n0v, n1v);
+        if (!BC_ABL(a.dbg, 4)) store_b(n0v, n1v, Bs, xs);
       }
       // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
       if (c + 2 < a.nchunks)
@@ -288,7 +318,10 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     }
   } else {
     const bool prio = BC_ABL(a.dbg, 16);
+    constexpr int DB_STORE = P == 2 ? 2 : 1;  // DB: K-step of chunk c that stores chunk c + 1
     for (int c = 0; c < a.nchunks; ++c) {
+      float xn = xs;  // DB: scale of chunk c + 1
+      if constexpr (DB) Br = Bs + (c & 1) * P * bplane;
       for (int tp = 0; tp < kst; ++tp) {
         const int step = c * kst + tp;
         if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
@@ -300,11 +333,23 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
           if (TPS == 1 || tap < K) compute(step & 1, tt, tap);
         }
         if (prio) __builtin_amdgcn_s_setprio(0);
-        if (tp == kst - 1 && c + 1 < a.nchunks) {
+        if constexpr (DB) {
+          // the idle buffer was last read in chunk c - 1 (every wave passed chunk c's first barrier)
+          if (c + 1 < a.nchunks) {
+            if (P == 2 && tp == 1) bmax_publish(bv0, bv1, (c + 1) & 1);  // read at step 2, after a barrier
+            if (tp == DB_STORE) {
+              if constexpr (P == 2) {
+                const float sn = bmax_scale((c + 1) & 1);
+                xn = sn < xs ? sn : xs;
+              }
+              if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1, Bs + ((c + 1) & 1) * P * bplane, xn);
+            }
+          }
+        } else if (tp == kst - 1 && c + 1 < a.nchunks) {
           if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
           if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-          if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1);
+          if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1, Bs, xs);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
         // step 0 of a multi-step chunk the 2*CI B loads of the next chunk were issued after it and
@@ -316,6 +361,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
       }
+      if constexpr (DB && P == 2) rescale_to(xn);  // chunk c's products are all in acc
     }
   }
 
@@ -357,9 +403,9 @@ inline constexpr X6Tile kX6Tiles[] = {
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
-inline size_t x6_lds(const X6Tile& t, int ncol, int planes, int s, int tps = 1) {
+inline size_t x6_lds(const X6Tile& t, int ncol, int planes, int s, int tps = 1, int bbufs = 1) {
   const size_t bplane = (size_t)((ncol * x6_pitch(s) + 15) / 16 * 16);
-  return planes * bplane + 2 * tps * planes * (size_t)t.WM * t.MT * 1024;
+  return bbufs * planes * bplane + 2 * tps * planes * (size_t)t.WM * t.MT * 1024;
 }
 
 // h3 and bf16 kernels run the multi-tap path with two taps per K-step where the doubled A buffers fit the
@@ -384,16 +430,36 @@ inline bool x6_pw_on() {
 // Which kernel variant a launch of tile t runs (shared by launch_x6 and bc_conv1d_kernel_name, so the
 // name the roofline reports is the one that ran): the pointwise two-chunk-prefetch path (K = 1), two taps
 // per K-step (h3 / bf16 multi-tap launches whose doubled A buffers fit), or one tap per K-step.
+// BC_X6_DB=0 disables the double-buffered B tile (A/B timing).
+inline bool x6_db_on() {
+  static const bool v = [] {
+    const char* e = getenv("BC_X6_DB");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 struct X6Variant {
   bool pw;
   int tps;
+  bool db;
+  size_t lds;
 };
 inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
   const int ncol = x6_ncol(t, K, s, d);
-  const size_t lds2 = x6_lds(t, ncol, P, s, 2);
-  if (K == 1 && ncol == x6_BN(t) && x6_pw_on()) return {true, 1};
-  if (P <= 2 && K > 1 && x6_tps() == 2 && (lds2 <= 80 * 1024 || (t.NT > 1 && lds2 <= 160 * 1024))) return {false, 2};
-  return {false, 1};
+  const size_t budget = t.NT > 1 ? 160 * 1024 : 80 * 1024;  // NT == 1: two workgroups per CU
+  auto fits = [&](int tps, int bb) { return x6_lds(t, ncol, P, s, tps, bb) <= budget; };
+  if (K == 1 && ncol == x6_BN(t) && x6_pw_on()) return {true, 1, false, x6_lds(t, ncol, P, s)};
+  const int min_kst = P == 2 ? 3 : 2;  // DB needs the store step after the maxima step
+  // preference (profiles/r02_x6_db.txt): two taps per K-step over the double B buffer (fewer barriers
+  // beat hidden staging: 192 x 256 k7 runs 2-3 % faster with TPS 2 than with DB at TPS 1); DB where only
+  // one tap per step fits (256 x 256: k7 768 -4.5 %, k3 1536 -6 %); NT == 1 tiles never (slower, spills)
+  const bool db = x6_db_on() && P <= 2 && t.NT > 1;
+  const bool tps2 = P <= 2 && K > 1 && x6_tps() == 2;
+  if (db && tps2 && (K + 1) / 2 >= min_kst && fits(2, 2)) return {false, 2, true, x6_lds(t, ncol, P, s, 2, 2)};
+  if (tps2 && fits(2, 1)) return {false, 2, false, x6_lds(t, ncol, P, s, 2)};
+  if (db && K >= min_kst && fits(1, 2)) return {false, 1, true, x6_lds(t, ncol, P, s, 1, 2)};
+  return {false, 1, false, x6_lds(t, ncol, P, s)};
 }
 
 template <int MT, int NT, int WM, int WN, int P>
@@ -418,15 +484,19 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
                  : nullptr;
   const size_t lds = x6_lds(t, ncol, P, a.s);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  const size_t lds2 = x6_lds(t, ncol, P, a.s, 2);
   const X6Variant v = x6_variant(t, P, a.K, a.s, a.d);
+  constexpr int T2 = P <= 2 ? 2 : 1;
+  constexpr bool D2 = P <= 2;
   if (v.pw)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), v.lds, st, a);
+  else if (v.db && v.tps == 2)
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2, D2>), dim3(a.nwg), dim3(512), v.lds, st, a);
+  else if (v.db)
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 1, D2>), dim3(a.nwg), dim3(512), v.lds, st, a);
   else if (v.tps == 2)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, (P <= 2 ? 2 : 1)>), dim3(a.nwg), dim3(512),
-                       lds2, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2>), dim3(a.nwg), dim3(512), v.lds, st, a);
   else
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), v.lds, st, a);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

@@ -256,11 +256,13 @@ def test_kernel_names_come_from_the_launchers():
             mt, nt, wm, wn = L.X6_CFGS[base % 100 + 100]
             planes = {1: 3, 2: 1, 3: 2}[base // 100]
             assert name.startswith(f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, "), (cfg, name)
-            assert name.endswith(("true, 1>", "false, 1>", "false, 2>")), name
+            # <..., planes, pointwise, taps per K-step, double-buffered B>
+            assert re.search(r", (true, 1, false|false, [12], (true|false))>$", name), name
         else:
             mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
             assert name == f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>", name
-    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1>")  # pointwise
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false>")  # pointwise
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3).endswith("false, 1, true>")
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_rr_kernel<48, 4, 1>"
     n96 = L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 3), 96, 3)
     assert n96.startswith("resunit_x6_kernel<") and ", 2, " in n96, n96
