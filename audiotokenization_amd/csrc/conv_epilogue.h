@@ -28,6 +28,9 @@ __device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, fl
 // (a power of two: exact) restores the fp32 dot product before the bias is added.
 // RP / rpre (MT == 1 only): the residual's 16-byte groups already loaded by the caller, one per n-tile,
 // for exactly the lanes / tiles that take the 16-byte path (conv_epilogue_res).
+// The 16-byte residual reads run one m-tile ahead of the m-tile being finished (two register sets):
+// issued next to the previous m-tile's arithmetic and stores instead of one dependent HBM round trip
+// per (m-tile, n-tile) (the pointwise convs' epilogue was a chain of MT x NT such round trips).
 template <int MT, int NT, bool SC, bool RP>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
                                                    int col0, int lane, float xinv, const floatx4 (&rpre)[NT]) {
@@ -35,8 +38,21 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
   float* y2b = a.y2 ? a.y2 + (long long)b * a.ybs : nullptr;
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
   const bool snk = a.osa != nullptr;
+  auto vec_tile = [&](int co, int nb) { return co < a.Cout && a.vec && nb + 3 < a.Nout; };
+  floatx4 rr[2][NT];
+  auto load_r = [&](int i, floatx4 (&d)[NT]) {
+    const int co = row0 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int nb = col0 + j * 16 + (lane >> 4) * 4;
+      d[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (rb && vec_tile(co, nb)) d[j] = *reinterpret_cast<const floatx4*>(rb + (long long)co * a.yT + a.ooff + nb);
+    }
+  };
+  if (!(MT == 1 && RP)) load_r(0, rr[0]);
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
+    if (!(MT == 1 && RP) && i + 1 < MT) load_r(i + 1, rr[(i + 1) & 1]);
     const int co = row0 + i * 16 + (lane & 15);
     if (co >= a.Cout) continue;
     const float bias = a.bias ? a.bias[co] : 0.f;
@@ -48,10 +64,9 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
     for (int j = 0; j < NT; ++j) {
       const int nb = col0 + j * 16 + (lane >> 4) * 4;
       if (nb >= a.Nout) continue;
-      if (a.vec && nb + 3 < a.Nout) {
+      if (vec_tile(co, nb)) {
         const long long yi = rowoff + nb;
-        floatx4 r = {0.f, 0.f, 0.f, 0.f};
-        if (rb) r = (MT == 1 && RP) ? rpre[j] : *reinterpret_cast<const floatx4*>(rb + yi);
+        const floatx4 r = (MT == 1 && RP) ? rpre[j] : rr[i & 1][j];
         floatx4 v, sv;
 #pragma unroll
         for (int q = 0; q < 4; ++q)

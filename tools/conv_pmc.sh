@@ -8,7 +8,9 @@ ARGS=${CONV_ARGS:---cin 192 --cout 192 --k 7 --d 3 --T 60000 --snake}
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM"
 i=0
-for ctr in "$P1" "$P2"; do
+P3="FETCH_SIZE"
+P4="WRITE_SIZE"
+for ctr in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/cpmc/p$i -o run -- \
     python3 tools/conv_bench.py --precision h3 --iters 3 $ARGS > gpurun_out/cpmc/p$i.log 2>&1
