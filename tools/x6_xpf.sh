@@ -1,0 +1,16 @@
+# Cross-unit operand prefetch (default) vs off (BC_X6_DEBUG=32), k7 h3 shapes.
+set -u
+mkdir -p gpurun_out
+out=gpurun_out/xpf.log
+: > $out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu \
+  > gpurun_out/xpf_tests.log 2>&1 || { echo "kernel tests failed"; tail -30 gpurun_out/xpf_tests.log; exit 1; }
+for dbg in 0 32 0 32; do
+  echo "== dbg $dbg" >> $out
+  run() { BC_X6_DEBUG=$dbg timeout -k 10 120 python tools/conv_bench.py --precision h3 --iters 5 "$@" >> $out 2>&1; }
+  run --cin 192 --cout 192 --k 7 --d 3 --T 60000 --snake || exit 1
+  run --cin 384 --cout 384 --k 7 --d 9 --T 30000 --snake || exit 1
+  run --cin 768 --cout 768 --k 7 --d 3 --T 6000 --snake || exit 1
+  run --cin 384 --cout 768 --k 10 --s 5 --T 6000 --dual || exit 1
+done
+grep -v amdgpu.ids $out
