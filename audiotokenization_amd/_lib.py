@@ -40,6 +40,8 @@ _SIGS = {
     "bc_lstm_workspace_floats": (L, [I, I, I]),
     "bc_reslstm_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
     "bc_reslstm_fwd_state": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P, P, P, P, P]),
+    "bc_reslstm_bidir_workspace_floats": (L, [I, I, I]),
+    "bc_reslstm_bidir_fwd": (I, [P, P, I, I, I, I, P, P, P, P, P, P, I, P]),
     "bc_vq_prepare_codebook": (I, [P, P, P, I, I, P]),
     "bc_vq_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P]),
     "bc_vq_argmin": (I, [P, P, P, P, L, I, I, P]),
@@ -58,7 +60,7 @@ _SIGS = {
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 8  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 9  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

@@ -235,46 +235,54 @@ class LSTM(nn.Module):
     def __init__(self, input_size, hidden_size, num_layers=1, bias=True, batch_first=True, dropout=0.0,
                  bidirectional=False):
         super().__init__()
-        if bidirectional:
-            raise NotImplementedError("bidirectional ResLSTM is not used by any shipped config")
         if not bias or not batch_first or dropout:
             raise NotImplementedError("only bias=True, batch_first=True, dropout=0")
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
         self.batch_first, self.bidirectional = batch_first, bidirectional
-        ref = nn.LSTM(input_size, hidden_size, num_layers, batch_first=True)  # torch's default init
+        ref = nn.LSTM(input_size, hidden_size, num_layers, batch_first=True,
+                      bidirectional=bidirectional)  # torch's default init and parameter names
         for name, p in ref.named_parameters():
             setattr(self, name, Parameter(p.detach().clone()))
         self._cache = _DeviceCache()
 
+    def _suffixes(self):
+        return ("", "_reverse") if self.bidirectional else ("",)
+
     def _plist(self):
         out = []
         for l in range(self.num_layers):
-            out += [getattr(self, f"weight_ih_l{l}"), getattr(self, f"weight_hh_l{l}"),
-                    getattr(self, f"bias_ih_l{l}"), getattr(self, f"bias_hh_l{l}")]
+            for sfx in self._suffixes():
+                out += [getattr(self, f"weight_ih_l{l}{sfx}"), getattr(self, f"weight_hh_l{l}{sfx}"),
+                        getattr(self, f"bias_ih_l{l}{sfx}"), getattr(self, f"bias_hh_l{l}{sfx}")]
         return out
 
     def prepared(self, device):
+        """Packed per-layer weights; bidirectional: [forward, backward] per layer (bc_reslstm_bidir_fwd)."""
         def build():
             lib = L.load()
             H = self.hidden_size
-            if self.input_size != H:
-                raise NotImplementedError("ResLSTM requires input_size == hidden_size")
+            # unidirectional: the residual needs input == hidden; bidirectional: every layer reads the
+            # 2H-channel concatenation, so the module input must be 2H as well
+            Cin = 2 * H if self.bidirectional else H
+            if self.input_size != Cin:
+                raise NotImplementedError("ResLSTM requires input_size == hidden_size (x2 when bidirectional)")
             mode = L.lstm_mode()
-            cfg = L.conv_cfg(4 * H, H, 1, 1, 1, mode)
+            cfg = L.conv_cfg(4 * H, Cin, 1, 1, 1, mode)
             wih, whh, bias = [], [], []
             for l in range(self.num_layers):
-                w = _cpu(getattr(self, f"weight_ih_l{l}")).contiguous()
-                packed = np.empty(L.checked_size(lib.bc_conv1d_packed_floats(4 * H, H, 1, cfg), "bc_conv1d_packed_floats"),
-                                  dtype=np.float32)
-                L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, H, 1, cfg)
-                wih.append(torch.from_numpy(packed).to(device))
-                w = _cpu(getattr(self, f"weight_hh_l{l}")).contiguous()
-                packed = np.empty(L.checked_size(lib.bc_lstm_hh_packed_floats(H, mode), "bc_lstm_hh_packed_floats"),
-                                  dtype=np.float32)
-                L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, mode)
-                whh.append(torch.from_numpy(packed).to(device))
-                b = _cpu(getattr(self, f"bias_ih_l{l}")) + _cpu(getattr(self, f"bias_hh_l{l}"))
-                bias.append(b.contiguous().to(device))
+                for sfx in self._suffixes():
+                    w = _cpu(getattr(self, f"weight_ih_l{l}{sfx}")).contiguous()
+                    packed = np.empty(L.checked_size(lib.bc_conv1d_packed_floats(4 * H, Cin, 1, cfg),
+                                                     "bc_conv1d_packed_floats"), dtype=np.float32)
+                    L.call("bc_conv1d_pack", w.numpy().ctypes.data, packed.ctypes.data, 4 * H, Cin, 1, cfg)
+                    wih.append(torch.from_numpy(packed).to(device))
+                    w = _cpu(getattr(self, f"weight_hh_l{l}{sfx}")).contiguous()
+                    packed = np.empty(L.checked_size(lib.bc_lstm_hh_packed_floats(H, mode), "bc_lstm_hh_packed_floats"),
+                                      dtype=np.float32)
+                    L.call("bc_lstm_pack_hh", w.numpy().ctypes.data, packed.ctypes.data, H, mode)
+                    whh.append(torch.from_numpy(packed).to(device))
+                    b = _cpu(getattr(self, f"bias_ih_l{l}{sfx}")) + _cpu(getattr(self, f"bias_hh_l{l}{sfx}"))
+                    bias.append(b.contiguous().to(device))
             arrs = (L.ptr_array([t.data_ptr() for t in wih]), L.ptr_array([t.data_ptr() for t in bias]),
                     L.ptr_array([t.data_ptr() for t in whh]))
             return (wih, whh, bias), arrs
@@ -300,6 +308,12 @@ class ResLSTM(nn.Module):
         B, H, T = x.shape
         (wih, whh, bias), _ = self.lstm.prepared(x.device)
         sa, sb = out_snake if out_snake is not None else (None, None)
+        if self.lstm.bidirectional:
+            if state is not None or return_state:
+                raise NotImplementedError("carried state (streaming) needs a unidirectional ResLSTM")
+            out = ops.load().reslstm_bidir(x, wih, bias, whh, sa, sb, L.precision_mode())
+            L.defer_status(out[1], f"ResLSTM(D={H}, layers={self.lstm.num_layers}, bidirectional, T={T})")
+            return out[0]
         h0, c0 = state if state is not None else (None, None)
         out = ops.load().reslstm(x, wih, bias, whh, sa, sb, L.precision_mode(), h0, c0, return_state)
         # include/bigcodec.h: out[1] = the call's count of persistent workgroups that timed out; the

@@ -223,6 +223,35 @@ int bc_reslstm_fwd_state(const float* x, float* out, int B, int H, int T, int nu
                       out_snake_inv_beta, workspace, mode, stream, h0, c0, hT, cT);
 }
 
+// One direction of one LSTM layer over a ctb sequence: gx = W_ih lin + b (k = 1 conv, Cin input
+// channels), then the recurrence into lout [H][T*B] (the persistent kernel, or one launch per step).
+static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const float* bias, const float* whh,
+                          float* lout, float* gx, float* cst, float* const (&frag)[2], int B, int H, int T, int mode,
+                          hipStream_t st, const float* h0, const float* c0, float* hT, float* cT, int* call_status) {
+  const long long tb = (long long)T * B;
+  if (!wih || !whh || !bias) return BC_ERR_ARG;
+  ConvArgs a{};
+  a.x = lin; a.w = wih; a.bias = bias; a.res = nullptr;
+  a.osa = nullptr; a.osb = nullptr; a.y = gx; a.y2 = nullptr;
+  a.xbs = 0; a.ybs = 0; a.rbs = 0;
+  a.Cin = Cin; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
+  a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
+  a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
+  int rc = conv_launch(a, 1, conv_select_cfg(4 * H, Cin, 1, 1, 1, mode), st);
+  if (rc) return rc;
+  if (lstm_use_seq(H, mode))  // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
+    return lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(whh), lout, cst, H, T, B, mode == 3 ? 2 : 3, st,
+                           h0, c0, hT, cT, call_status);
+  if (h0 || c0 || hT || cT) return BC_ERR_UNSUPPORTED;  // carried state: the persistent kernel only
+  const bool fast = lstm_fast_ok(H);
+  for (int t = 0; t < T; ++t) {
+    rc = fast ? lstm_step_frag_launch(gx, whh, frag[(t + 1) & 1], frag[t & 1], lout, cst, H, B, T, t, st)
+              : lstm_step_launch(gx, whh, lout, cst, H, B, T, t, st);
+    if (rc) return rc;
+  }
+  return BC_OK;
+}
+
 static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num_layers,
                         const float* const* w_ih_packed, const float* const* bias,
                         const float* const* w_hh_packed, const float* out_snake_alpha_exp,
@@ -231,7 +260,6 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
   if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || H <= 0 ||
       H % 16 || T < 0 || num_layers <= 0 || mode < 0 || mode > 3)
     return BC_ERR_ARG;
-  const bool state = h0 || c0 || hT || cT;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   hipStream_t st = S(stream);
   int* call_status = reinterpret_cast<int*>(workspace);  // workspace[0]: this call's timeout count
@@ -245,46 +273,77 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
   float* ya = gx + tb * 4 * H;
   float* yb = ya + tb * H;
   float* cst = yb + tb * H;
-  float* frag[2] = {cst + (long long)H * B, cst + (long long)H * B + lstm_frag_floats(B, H)};
-  const bool fast = lstm_fast_ok(H);
+  float* const frag[2] = {cst + (long long)H * B, cst + (long long)H * B + lstm_frag_floats(B, H)};
   int rc = btc_to_ctb_launch(x, xt, B, H, T, st);
   if (rc) return rc;
-  const int cfg = conv_select_cfg(4 * H, H, 1, 1, 1, mode);
   const float* lin = xt;
   float* lout = ya;
   for (int l = 0; l < num_layers; ++l) {
-    if (!w_ih_packed[l] || !w_hh_packed[l] || !bias[l]) return BC_ERR_ARG;
-    ConvArgs a{};
-    a.x = lin; a.w = w_ih_packed[l]; a.bias = bias[l]; a.res = nullptr;
-    a.osa = nullptr; a.osb = nullptr; a.y = gx; a.y2 = nullptr;
-    a.xbs = 0; a.ybs = 0; a.rbs = 0;
-    a.Cin = H; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
-    a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
-    a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
-    rc = conv_launch(a, 1, cfg, st);
+    const long long so = (long long)l * H * B;  // layer l's [H][B] state
+    rc = lstm_layer_dir(lin, H, w_ih_packed[l], bias[l], w_hh_packed[l], lout, gx, cst, frag, B, H, T, mode, st,
+                        h0 ? h0 + so : nullptr, c0 ? c0 + so : nullptr, hT ? hT + so : nullptr,
+                        cT ? cT + so : nullptr, call_status);
     if (rc) return rc;
-    if (lstm_use_seq(H, mode)) {
-      // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
-      const long long so = (long long)l * H * B;  // layer l's [H][B] state
-      rc = lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(w_hh_packed[l]), lout, cst, H, T, B,
-                           mode == 3 ? 2 : 3, st, h0 ? h0 + so : nullptr, c0 ? c0 + so : nullptr,
-                           hT ? hT + so : nullptr, cT ? cT + so : nullptr, call_status);
-      if (rc) return rc;
-      lin = lout;
-      lout = (lout == ya) ? yb : ya;
-      continue;
-    }
-    if (state) return BC_ERR_UNSUPPORTED;  // carried state: the persistent kernel only
-    for (int t = 0; t < T; ++t) {
-      rc = fast ? lstm_step_frag_launch(gx, w_hh_packed[l], frag[(t + 1) & 1], frag[t & 1], lout, cst,
-                                        H, B, T, t, st)
-                : lstm_step_launch(gx, w_hh_packed[l], lout, cst, H, B, T, t, st);
-      if (rc) return rc;
-    }
     lin = lout;
     lout = (lout == ya) ? yb : ya;
   }
   return ctb_to_btc_add_launch(lin, x, out_snake_alpha_exp, out_snake_inv_beta, out, B, H, T, st);
+}
+
+// Bidirectional ResLSTM (vq/module.py:150-152 with bidirectional=True: nn.LSTM(D, D / 2, bidirectional)):
+// per layer the forward direction writes channels [0, H) of the layer output and the backward
+// direction, run as the forward recurrence over the time-reversed input and reversed back, channels
+// [H, 2H) (torch's concatenation order); every layer's input has D = 2H channels.
+// workspace: status | xt [D][T*B] | gx [4H][T*B] | cat0, cat1 [D][T*B] | rin [D][T*B] | rout [H][T*B] |
+// c [H][B] | hfrag x2 or the persistent kernel's region
+long long bc_reslstm_bidir_workspace_floats(int B, int D, int T) {
+  if (B < 0 || D <= 0 || D % 32 || T < 0) return -1;
+  const int H = D / 2;
+  const long long tb = (long long)T * B;
+  const long long frag = 2 * lstm_frag_floats(B, H);
+  const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
+  return LSTM_WS_STATUS_FLOATS + tb * D * 4 + tb * 4 * H + tb * H + (long long)H * B + (frag > seq ? frag : seq);
+}
+
+int bc_reslstm_bidir_fwd(const float* x, float* out, int B, int D, int T, int num_layers,
+                         const float* const* w_ih_packed, const float* const* bias, const float* const* w_hh_packed,
+                         const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* workspace, int mode,
+                         void* stream) {
+  if (!x || !out || !w_ih_packed || !bias || !w_hh_packed || !workspace || B < 0 || D <= 0 || D % 32 || T < 0 ||
+      num_layers <= 0 || mode < 0 || mode > 3)
+    return BC_ERR_ARG;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  hipStream_t st = S(stream);
+  int* call_status = reinterpret_cast<int*>(workspace);
+  if (hipMemsetAsync(call_status, 0, sizeof(int), st) != hipSuccess) return BC_ERR_LAUNCH;
+  if (B == 0 || T == 0) return BC_OK;
+  mode = lstm_mode(mode);
+  const int H = D / 2;
+  const long long tb = (long long)T * B;
+  if (tb > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  float* xt = workspace + LSTM_WS_STATUS_FLOATS;
+  float* gx = xt + tb * D;
+  float* cat[2] = {gx + tb * 4 * H, gx + tb * 4 * H + tb * D};
+  float* rin = cat[1] + tb * D;
+  float* rout = rin + tb * D;
+  float* cst = rout + tb * H;
+  float* const frag[2] = {cst + (long long)H * B, cst + (long long)H * B + lstm_frag_floats(B, H)};
+  int rc = btc_to_ctb_launch(x, xt, B, D, T, st);
+  if (rc) return rc;
+  const float* lin = xt;
+  for (int l = 0; l < num_layers; ++l) {
+    float* y = cat[l & 1];
+    rc = lstm_layer_dir(lin, D, w_ih_packed[2 * l], bias[2 * l], w_hh_packed[2 * l], y, gx, cst, frag, B, H, T, mode,
+                        st, nullptr, nullptr, nullptr, nullptr, call_status);
+    if (rc) return rc;
+    if ((rc = time_reverse_launch(lin, rin, D, T, B, st))) return rc;
+    rc = lstm_layer_dir(rin, D, w_ih_packed[2 * l + 1], bias[2 * l + 1], w_hh_packed[2 * l + 1], rout, gx, cst, frag,
+                        B, H, T, mode, st, nullptr, nullptr, nullptr, nullptr, call_status);
+    if (rc) return rc;
+    if ((rc = time_reverse_launch(rout, y + tb * H, H, T, B, st))) return rc;
+    lin = y;
+  }
+  return ctb_to_btc_add_launch(lin, x, out_snake_alpha_exp, out_snake_inv_beta, out, B, D, T, st);
 }
 
 int bc_vq_prepare_codebook(const float* codebook, float* codebook_norm, float* codebook_sq,

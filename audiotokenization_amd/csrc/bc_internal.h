@@ -68,6 +68,7 @@ int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, co
                           float* out, int B, int C, int T, hipStream_t st);
 int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st);
 int tanh_launch(const float* x, float* y, long long n, hipStream_t st);
+int time_reverse_launch(const float* x, float* y, int C, int T, int B, hipStream_t st);
 
 bool lstm_fast_ok(int H);
 void lstm_pack_hh2(const float* w, float* out, int H);

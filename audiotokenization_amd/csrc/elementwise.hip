@@ -214,6 +214,36 @@ int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, co
   return BC_OK;
 }
 
+// [C][T][B] -> [C][T][B] with time reversed (the backward direction of a bidirectional LSTM runs the
+// forward recurrence over the reversed sequence); B floats per (c, t) row, 16-byte moves when B % 4 == 0.
+__global__ void time_reverse_kernel(const float* __restrict__ x, float* __restrict__ y, long long rows, int T, int B) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (B % 4 == 0) {
+    const int q = B / 4;
+    const long long n = rows * q;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+      const long long row = e / q, c = row / T;
+      const int t = (int)(row - c * T), j = (int)(e - row * q);
+      reinterpret_cast<float4*>(y)[(c * T + (T - 1 - t)) * q + j] = reinterpret_cast<const float4*>(x)[e];
+    }
+    return;
+  }
+  const long long n = rows * B;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const long long row = e / B, c = row / T;
+    const int t = (int)(row - c * T), b = (int)(e - row * B);
+    y[(c * T + (T - 1 - t)) * B + b] = x[e];
+  }
+}
+
+int time_reverse_launch(const float* x, float* y, int C, int T, int B, hipStream_t st) {
+  const long long rows = (long long)C * T, n = rows * (B % 4 == 0 ? B / 4 : B);
+  if (n == 0) return BC_OK;
+  hipLaunchKernelGGL(time_reverse_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, x, y, rows, T, B);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
 int tanh_launch(const float* x, float* y, long long n, hipStream_t st) {
   if (n == 0) return BC_OK;
   hipLaunchKernelGGL(tanh_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, x, y, n);

@@ -190,6 +190,34 @@ Tensor tanh_op(const Tensor& x) {
   return y;
 }
 
+// ---- bidirectional ResLSTM: [y, status]; w_* hold [forward, backward] per layer ----------------------------------
+std::vector<Tensor> reslstm_bidir(const Tensor& x, at::TensorList w_ih, at::TensorList bias, at::TensorList w_hh,
+                                  const optional<Tensor>& sa, const optional<Tensor>& sb, int64_t mode) {
+  dev(x, "x");
+  TORCH_CHECK_VALUE(x.dim() == 3, "bigcodec::reslstm_bidir: x must be (B, D, T)");
+  const int64_t n = (int64_t)w_ih.size();
+  TORCH_CHECK_VALUE(n > 0 && n % 2 == 0 && (int64_t)bias.size() == n && (int64_t)w_hh.size() == n,
+                    "bigcodec::reslstm_bidir: w_ih / bias / w_hh hold [forward, backward] per layer");
+  const int B = i32(x.size(0), "B"), D = i32(x.size(1), "D"), T = i32(x.size(2), "T");
+  check_coeffs(sa, sb, D, "reslstm_bidir out snake");
+  std::vector<const float*> pih, pb, phh;
+  for (int64_t l = 0; l < n; ++l) {
+    pih.push_back(req(x, w_ih[l], "w_ih_packed[l]"));
+    pb.push_back(req(x, bias[l], "bias[l]"));
+    phh.push_back(req(x, w_hh[l], "w_hh_packed[l]"));
+  }
+  const long long nws = bc_reslstm_bidir_workspace_floats(B, D, T);
+  TORCH_CHECK_VALUE(nws >= 0, "bigcodec::reslstm_bidir: unsupported shape (D % 32 != 0)");
+  auto ws = at::empty({std::max<long long>(nws, 64)}, x.options());
+  auto y = at::empty_like(x);
+  ok(bc_reslstm_bidir_fwd(x.data_ptr<float>(), y.data_ptr<float>(), B, D, T, (int)(n / 2), pih.data(), pb.data(),
+                          phh.data(), optf(x, sa, "out_alpha_exp"), optf(x, sb, "out_inv_beta"), ws.data_ptr<float>(),
+                          i32(mode, "mode"), stream_of(x)),
+     "bc_reslstm_bidir_fwd");
+  Tensor status = ws.narrow(0, 0, 1).view(at::kInt).clone();
+  return {y, status};
+}
+
 // ---- ResLSTM: returns [y, status] (+ [hT, cT]); status = the call's int32 timeout count --------------------------
 std::vector<Tensor> reslstm(const Tensor& x, at::TensorList w_ih, at::TensorList bias, at::TensorList w_hh,
                             const optional<Tensor>& sa, const optional<Tensor>& sb, int64_t mode,
@@ -387,6 +415,8 @@ TORCH_LIBRARY(bigcodec, m) {
   m.def("tanh(Tensor x) -> Tensor");
   m.def("reslstm(Tensor x, Tensor[] w_ih_packed, Tensor[] bias, Tensor[] w_hh_packed, Tensor? out_alpha_exp, "
         "Tensor? out_inv_beta, int mode, Tensor? h0, Tensor? c0, bool return_state) -> Tensor[]");
+  m.def("reslstm_bidir(Tensor x, Tensor[] w_ih_packed, Tensor[] bias, Tensor[] w_hh_packed, Tensor? out_alpha_exp, "
+        "Tensor? out_inv_beta, int mode) -> Tensor[]");
   m.def("vq_prepare_codebook(Tensor codebook) -> Tensor[]");
   m.def("vq(Tensor z, Tensor w_in, Tensor b_in, Tensor codebook, Tensor codebook_norm, Tensor codebook_sq, "
         "Tensor w_out, Tensor b_out, bool want_ze, bool want_post) -> Tensor[]");
@@ -408,6 +438,7 @@ TORCH_LIBRARY_IMPL(bigcodec, CUDA, m) {
   m.impl("aa_snake", &aa_snake);
   m.impl("tanh", &tanh_op);
   m.impl("reslstm", &reslstm);
+  m.impl("reslstm_bidir", &reslstm_bidir);
   m.impl("vq_prepare_codebook", &vq_prepare_codebook);
   m.impl("vq", &vq);
   m.impl("vq_argmin", &vq_argmin);

@@ -24,7 +24,7 @@ _lock = threading.Lock()
 _ns = None
 
 # every op the extension defines (tests check the registry against this list)
-OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "tanh", "reslstm", "vq_prepare_codebook", "vq",
+OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "tanh", "reslstm", "reslstm_bidir", "vq_prepare_codebook", "vq",
        "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "resample_sinc", "synth_clips_")
 
 
@@ -87,6 +87,10 @@ def _register_fakes():
             B, H, _ = x.shape
             out += [_new(x, (len(w_ih), H, B)), _new(x, (len(w_ih), H, B))]
         return out
+
+    @reg("bigcodec::reslstm_bidir")
+    def _reslstm_bidir(x, w_ih, bias, w_hh, sa, sb, mode):
+        return [_new(x, x.shape), _new(x, (1,), torch.int32)]
 
     @reg("bigcodec::vq_prepare_codebook")
     def _prep(cb):

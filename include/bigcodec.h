@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 8
+#define BC_ABI_VERSION 9
 
 int bc_abi_version(void);
 
@@ -168,6 +168,21 @@ int bc_reslstm_fwd_state(const float* x, float* out, int B, int H, int T, int nu
                          const float* const* w_hh_packed, const float* out_snake_alpha_exp,
                          const float* out_snake_inv_beta, float* workspace, int mode, const float* h0,
                          const float* c0, float* hT, float* cT, void* stream);
+
+/* bc_reslstm_bidir_fwd: ResLSTM(dimension = D, bidirectional=True) (vq/module.py:150-152: nn.LSTM(D, D / 2,
+ *   num_layers, batch_first=True, bidirectional=True)), + skip.  x, out: [B][D][T], H = D / 2, D % 32 == 0.
+ *   The pointer arrays hold TWO entries per layer, [2l] = forward and [2l + 1] = backward direction
+ *   (torch's weight_ih_l{l} / weight_ih_l{l}_reverse ...), each packed as above but with Cin = D:
+ *   w_ih_packed = bc_conv1d_pack(weight_ih as [4H][D][1], cfg = bc_conv1d_select_cfg(4H, D, 1, 1, 1, mode)),
+ *   w_hh_packed = bc_lstm_pack_hh(weight_hh, H, mode).  Layer outputs are [forward h | backward h]
+ *   (torch's concatenation order); the backward direction runs the forward recurrence over the
+ *   time-reversed sequence.  workspace: bc_reslstm_bidir_workspace_floats(B, D, T) floats, same timeout
+ *   status contract as bc_reslstm_fwd.  No carried state (streaming models are unidirectional). */
+long long bc_reslstm_bidir_workspace_floats(int B, int D, int T);
+int bc_reslstm_bidir_fwd(const float* x, float* out, int B, int D, int T, int num_layers,
+                         const float* const* w_ih_packed, const float* const* bias,
+                         const float* const* w_hh_packed, const float* out_snake_alpha_exp,
+                         const float* out_snake_inv_beta, float* workspace, int mode, void* stream);
 
 /* ---- Factorized VQ (codebook_dim == 8) ---------------------------------------------------------
  * bc_vq_prepare_codebook: F.normalize(codebook) and its row sums of squares

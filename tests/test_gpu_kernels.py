@@ -482,3 +482,31 @@ def test_lstm_timeout_is_loud(dev):
         again = enc(x)
         torch.cuda.synchronize()
     assert torch.equal(good, again)
+    assert lib.bc_lstm_status(1) > 0  # the process-wide diagnostic saw them (reset for later tests)
+
+
+@pytest.mark.parametrize("D,layers,B,T", [(64, 2, 3, 37), (512, 2, 4, 50), (1536, 1, 2, 23)])
+def test_reslstm_bidirectional(dev, D, layers, B, T):
+    """ResLSTM(bidirectional=True) (vq/module.py:150-152: nn.LSTM(D, D/2, bidirectional)) against torch's
+    own CPU LSTM (oracle.res_lstm): D = 64 runs the per-step kernels (H = 32), D = 512 / 1536 the
+    persistent one (H = 256 / 768) for both directions; plus the fused output Snake."""
+    L.load().bc_lstm_status(1)
+    g = torch.Generator().manual_seed(D + T)
+    m = BL.ResLSTM(D, num_layers=layers, bidirectional=True)
+    H = D // 2
+    with torch.no_grad():
+        for p in m.lstm.parameters():
+            p.copy_((torch.rand(p.shape, generator=g) * 2 - 1) / np.sqrt(H))
+    assert any(k.endswith("_reverse") for k in m.state_dict())  # torch's parameter names (checkpoint keys)
+    x = torch.randn(B, D, T, generator=g)
+    sd = {k: v.detach() for k, v in m.state_dict().items()}
+    want = O.res_lstm(x, sd, "", layers, bidirectional=True)
+    got = m.to(dev)(x.to(dev)).cpu()
+    assert_close_rel(got, want, 2e-5, f"bidirectional lstm D={D}")
+    snake = _snake(D, g).to(dev)
+    got_s = m.run(x.to(dev), out_snake=snake.coeffs(dev)).cpu()
+    want_s = O.snake_beta(want, snake.alpha.detach().cpu(), snake.beta.detach().cpu())
+    assert_close_rel(got_s, want_s, 5e-5, f"bidirectional lstm+snake D={D}")
+    with pytest.raises(NotImplementedError):
+        m.run(x.to(dev), return_state=True)
+    assert L.load().bc_lstm_status(1) == 0

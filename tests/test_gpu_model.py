@@ -207,3 +207,18 @@ def test_rvq_multi_quantizer_against_reference(dev, golden, nq):
             wq = torch.from_numpy(g["post"]).permute(0, 2, 1).reshape(-1, post.shape[1])[ok]
             assert_close_rel(gq, wq, 1e-5, f"rvq nq={nq} post")
     assert_close_rel(emb.cpu(), torch.from_numpy(g["vq2emb"]), 1e-6, f"rvq nq={nq} vq2emb")
+
+
+def test_bidirectional_rnn_encoder_against_oracle(dev):
+    """rnn_bidirectional=True (codec_encoder.py:18,46, a constructor option no shipped config sets): the
+    'base' encoder with a bidirectional ResLSTM against the CPU oracle (torch's LSTM inside)."""
+    enc, dec, esd, dsd, ek, dk = build_models("base", device=dev, rnn_bidirectional=True)
+    assert ek["rnn_bidirectional"]
+    from audiotokenization_amd import synth
+
+    x = torch.from_numpy(synth.synth_clips(2, 9600, clip0=11)).unsqueeze(1)
+    with torch.no_grad():
+        lat_ref = O.encoder_forward(x, torch_sd(esd), ek)
+        lat = enc(x.to(dev))
+        torch.cuda.synchronize()
+    assert_close_rel(lat.cpu(), lat_ref, 1e-4, "bidirectional-rnn latent")

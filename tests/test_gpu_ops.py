@@ -48,6 +48,10 @@ def _cases(dev, base):
     (wih, whh, lb), _ = lstm.lstm.prepared(dev)
     xl = torch.randn(2, H, 9, generator=g).to(dev)
     cases.append(("reslstm", (xl, wih, lb, whh, None, None, L.precision_mode(), None, None, True)))
+    bl = ResLSTM(64, num_layers=1, bidirectional=True).to(dev)
+    (bwih, bwhh, bb), _ = bl.lstm.prepared(dev)
+    cases.append(("reslstm_bidir", (torch.randn(2, 64, 7, generator=g).to(dev), bwih, bb, bwhh, None, None,
+                                    L.precision_mode())))
     fvq = dec.quantizer.layers[0]
     cb, cbn, csq, w_in, b_in, w_out, b_out = fvq.prepared(dev)
     z = torch.randn(2, fvq.dim, 11, generator=g).to(dev)
@@ -68,7 +72,7 @@ def test_opcheck_every_codec_op(dev, base):
     for name, args in _cases(dev, base):
         torch.library.opcheck(getattr(ns, name).default, args)
         seen.add(name)
-    assert {"conv1d", "snake", "tanh", "reslstm", "vq", "vq2emb", "vq2emb_ct"} <= seen
+    assert {"conv1d", "snake", "tanh", "reslstm", "reslstm_bidir", "vq", "vq2emb", "vq2emb_ct"} <= seen
 
 
 def test_ops_equal_the_raw_c_abi(dev, base):
