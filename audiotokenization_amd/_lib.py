@@ -33,6 +33,8 @@ _SIGS = {
     "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
     "bc_aa_snake_fwd": (I, [P, P, P, P, P, P, I, I, I, P]),
+    "bc_aa_snake_out_len": (L, [I, I, I, I]),
+    "bc_aa_snake_fwd_ex": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, P]),
     "bc_lstm_hh_packed_floats": (L, [I, I]),
     "bc_lstm_pack_hh": (I, [P, P, I, I]),
     "bc_lstm_status": (I, [I]),

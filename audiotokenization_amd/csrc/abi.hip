@@ -150,6 +150,23 @@ int bc_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snak
   return snake_launch(x, snake_alpha_exp, snake_inv_beta, y, B, C, T, S(stream));
 }
 
+long long bc_aa_snake_out_len(int T, int up_ratio, int down_ratio, int down_taps) {
+  if (T < 0 || up_ratio < 1 || down_ratio < 1 || down_taps < 1) return -1;
+  return aa_snake_out_len(T, up_ratio, down_ratio, down_taps);
+}
+
+int bc_aa_snake_fwd_ex(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                       const float* up_filter, const float* down_filter, float* y, int B, int C, int T, int up_ratio,
+                       int up_taps, int down_ratio, int down_taps, void* stream) {
+  if (!x || !y || !snake_alpha_exp || !snake_inv_beta || !up_filter || !down_filter || B < 0 || C <= 0 || T < 0 ||
+      up_ratio < 1 || down_ratio < 1 || up_taps < 1 || down_taps < 1)
+    return BC_ERR_ARG;
+  if (up_ratio == 2 && down_ratio == 2 && up_taps == 12 && down_taps == 12)  // the reference's default: fixed kernel
+    return aa_snake_launch(x, snake_alpha_exp, snake_inv_beta, up_filter, down_filter, y, B, C, T, S(stream));
+  return aa_snake_gen_launch(x, snake_alpha_exp, snake_inv_beta, up_filter, down_filter, y, B, C, T, up_ratio, up_taps,
+                             down_ratio, down_taps, S(stream));
+}
+
 int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
                     const float* up_filter, const float* down_filter, float* y, int B, int C, int T,
                     void* stream) {

@@ -69,6 +69,9 @@ int ctb_to_btc_add_launch(const float* y, const float* skip, const float* sa, co
 int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_t st);
 int tanh_launch(const float* x, float* y, long long n, hipStream_t st);
 int time_reverse_launch(const float* x, float* y, int C, int T, int B, hipStream_t st);
+long long aa_snake_out_len(int T, int ru, int rd, int kd);
+int aa_snake_gen_launch(const float* x, const float* sa, const float* sb, const float* fu, const float* fd, float* y,
+                        int B, int C, int T, int ru, int ku, int rd, int kd, hipStream_t st);
 
 bool lstm_fast_ok(int H);
 void lstm_pack_hh2(const float* w, float* out, int H);

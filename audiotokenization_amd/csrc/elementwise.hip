@@ -185,6 +185,97 @@ int snake_launch(const float* x, const float* sa, const float* sb, float* y, int
   return BC_OK;
 }
 
+// Activation1d with any (up_ratio, up taps, down_ratio, down taps) (act.py:8-23 constructor arguments):
+// the same three stages as aa_snake_kernel, with the geometry of resample.py:10-33 / filter.py:86-95 at
+// run time.  Up: replicate pad P = Ku / ru - 1, transposed conv stride ru, x ru, crop [PL, -PR) with
+// PL = P ru + (Ku - ru) / 2; Snake; down: replicate pad (Kd / 2 - even, Kd / 2), conv stride rd.
+// One workgroup = AA_TILE outputs of one (b, c) row; the tile's snake values s[j] (j = t rd + k - DL)
+// and the x range they need sit in dynamic LDS.
+__global__ void __launch_bounds__(256) aa_snake_gen_kernel(const float* __restrict__ x, const float* __restrict__ sa,
+                                                           const float* __restrict__ sb, const float* __restrict__ fup,
+                                                           const float* __restrict__ fdown, float* __restrict__ y,
+                                                           int C, int T, int Tout, int ntiles, int ru, int ku, int rd,
+                                                           int kd, int nx, int ns) {
+  extern __shared__ float aa_sm[];
+  float* fu = aa_sm;
+  float* fd = fu + ku;
+  float* xl = fd + kd;
+  float* sl = xl + nx;
+  const int tile = blockIdx.x % ntiles;
+  const long long row = blockIdx.x / ntiles;  // b*C + c
+  const int c = (int)(row % C);
+  const float* xr = x + row * T;
+  float* yr = y + row * (long long)Tout;
+  const int t0 = tile * AA_TILE;
+  const long long L = (long long)T * ru;            // up-sampled length
+  const int up_pad = ku / ru - 1;
+  const int up_pl = up_pad * ru + (ku - ru) / 2;    // crop offset into the transposed-conv output
+  const int dn_pl = kd / 2 - (kd % 2 == 0 ? 1 : 0);
+  for (int e = threadIdx.x; e < ku; e += 256) fu[e] = fup[e];
+  for (int e = threadIdx.x; e < kd; e += 256) fd[e] = fdown[e];
+  // s index range of the tile: j = t rd + k - dn_pl, clamped to [0, L) (replicate pad of the Snake output)
+  const long long j0 = (long long)t0 * rd - dn_pl;
+  const long long v0 = j0 < 0 ? 0 : (j0 >= L ? L - 1 : j0);
+  // transposed-conv input indices i = (v + up_pl - k) / ru over the clamped v range
+  const long long ibase = (v0 + up_pl - (ku - 1)) / ru - 1;
+  for (int e = threadIdx.x; e < nx; e += 256) {
+    long long xi = ibase + e - up_pad;  // padded index -> x index, replicate
+    xi = xi < 0 ? 0 : (xi >= T ? T - 1 : xi);
+    xl[e] = xr[xi];
+  }
+  __syncthreads();
+  const float a = sa[c], ib = sb[c];
+  const long long np = (long long)T + 2 * up_pad;  // padded input length
+  for (int e = threadIdx.x; e < ns; e += 256) {
+    long long v = j0 + e;
+    v = v < 0 ? 0 : (v >= L ? L - 1 : v);
+    const long long u = v + up_pl;
+    float acc = 0.f;
+    for (int k = (int)(u % ru); k < ku; k += ru) {  // out[u] = sum_{k: (u - k) % ru == 0} x_p[(u - k) / ru] f[k]
+      const long long i = (u - k) / ru;
+      if (i >= np) continue;
+      if (i < 0) break;
+      acc = acc + xl[i - ibase] * fu[k];
+    }
+    sl[e] = snake((float)ru * acc, a, ib);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < AA_TILE; e += 256) {
+    const int t = t0 + e;
+    if (t >= Tout) break;
+    float acc = 0.f;
+    for (int k = 0; k < kd; ++k) acc = acc + sl[e * rd + k] * fd[k];
+    yr[t] = acc;
+  }
+}
+
+// output length of the general activation (the down stage's conv over the padded up-sampled signal)
+long long aa_snake_out_len(int T, int ru, int rd, int kd) {
+  const long long L = (long long)T * ru;
+  const int pl = kd / 2 - (kd % 2 == 0 ? 1 : 0), pr = kd / 2;
+  const long long n = L + pl + pr - kd;
+  return n < 0 ? 0 : n / rd + 1;
+}
+
+int aa_snake_gen_launch(const float* x, const float* sa, const float* sb, const float* fu, const float* fd, float* y,
+                        int B, int C, int T, int ru, int ku, int rd, int kd, hipStream_t st) {
+  if (ru < 1 || rd < 1 || ku < ru || kd < 1 || ku > 256 || kd > 256 || ru > 16 || rd > 16) return BC_ERR_UNSUPPORTED;
+  const long long Tout = aa_snake_out_len(T, ru, rd, kd);
+  if ((long long)B * C * T == 0 || Tout == 0) return BC_OK;
+  if (Tout > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  const int ntiles = (int)((Tout + AA_TILE - 1) / AA_TILE);
+  const long long nwg = (long long)B * C * ntiles;
+  if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
+  const int ns = (AA_TILE - 1) * rd + kd;
+  const int nx = (ns + ku) / ru + 4;
+  const size_t lds = (size_t)(ku + kd + nx + ns) * sizeof(float);
+  if (lds > 64 * 1024) return BC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(aa_snake_gen_kernel, dim3((unsigned)nwg), dim3(256), lds, st, x, sa, sb, fu, fd, y, C, T,
+                     (int)Tout, ntiles, ru, ku, rd, kd, nx, ns);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
 int aa_snake_launch(const float* x, const float* sa, const float* sb, const float* fu,
                     const float* fd, float* y, int B, int C, int T, hipStream_t st) {
   if ((long long)B * C * T == 0) return BC_OK;

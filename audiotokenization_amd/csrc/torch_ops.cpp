@@ -190,6 +190,23 @@ Tensor tanh_op(const Tensor& x) {
   return y;
 }
 
+Tensor aa_snake_ex(const Tensor& x, const Tensor& a, const Tensor& ib, const Tensor& fu, const Tensor& fd,
+                   int64_t up_ratio, int64_t down_ratio) {
+  dev(x, "x");
+  TORCH_CHECK_VALUE(x.dim() == 3, "bigcodec::aa_snake_ex: x must be (B, C, T)");
+  TORCH_CHECK_VALUE(a.numel() == x.size(1) && ib.numel() == x.size(1), "bigcodec::aa_snake_ex: coefficients must have C entries");
+  const int T = i32(x.size(2), "T"), ru = i32(up_ratio, "up_ratio"), rd = i32(down_ratio, "down_ratio");
+  const int ku = i32(fu.numel(), "up taps"), kd = i32(fd.numel(), "down taps");
+  const long long Tout = bc_aa_snake_out_len(T, ru, rd, kd);
+  TORCH_CHECK_VALUE(Tout >= 0, "bigcodec::aa_snake_ex: bad ratios");
+  auto y = at::empty({x.size(0), x.size(1), (int64_t)Tout}, x.options());
+  ok(bc_aa_snake_fwd_ex(x.data_ptr<float>(), req(x, a, "alpha_exp"), req(x, ib, "inv_beta"), req(x, fu, "up_filter"),
+                        req(x, fd, "down_filter"), y.data_ptr<float>(), i32(x.size(0), "B"), i32(x.size(1), "C"), T, ru,
+                        ku, rd, kd, stream_of(x)),
+     "bc_aa_snake_fwd_ex");
+  return y;
+}
+
 // ---- bidirectional ResLSTM: [y, status]; w_* hold [forward, backward] per layer ----------------------------------
 std::vector<Tensor> reslstm_bidir(const Tensor& x, at::TensorList w_ih, at::TensorList bias, at::TensorList w_hh,
                                   const optional<Tensor>& sa, const optional<Tensor>& sb, int64_t mode) {
@@ -412,6 +429,8 @@ TORCH_LIBRARY(bigcodec, m) {
         "Tensor? out_inv_beta, int dilation, int pad_left, int cfg, bool dual) -> Tensor[]");
   m.def("snake(Tensor x, Tensor alpha_exp, Tensor inv_beta) -> Tensor");
   m.def("aa_snake(Tensor x, Tensor alpha_exp, Tensor inv_beta, Tensor up_filter, Tensor down_filter) -> Tensor");
+  m.def("aa_snake_ex(Tensor x, Tensor alpha_exp, Tensor inv_beta, Tensor up_filter, Tensor down_filter, int up_ratio, "
+        "int down_ratio) -> Tensor");
   m.def("tanh(Tensor x) -> Tensor");
   m.def("reslstm(Tensor x, Tensor[] w_ih_packed, Tensor[] bias, Tensor[] w_hh_packed, Tensor? out_alpha_exp, "
         "Tensor? out_inv_beta, int mode, Tensor? h0, Tensor? c0, bool return_state) -> Tensor[]");
@@ -437,6 +456,7 @@ TORCH_LIBRARY_IMPL(bigcodec, CUDA, m) {
   m.impl("snake", &snake);
   m.impl("aa_snake", &aa_snake);
   m.impl("tanh", &tanh_op);
+  m.impl("aa_snake_ex", &aa_snake_ex);
   m.impl("reslstm", &reslstm);
   m.impl("reslstm_bidir", &reslstm_bidir);
   m.impl("vq_prepare_codebook", &vq_prepare_codebook);

@@ -220,7 +220,8 @@ class DownSample1d(nn.Module):
 
 class Activation1d(nn.Module):
     """vq/alias_free_torch/act.py:7-32.  Without antialias the Snake alone; with antialias the fused
-    up(2x, 12 taps) -> Snake -> down(2x, 12 taps) kernel."""
+    up -> Snake -> down kernel (the default 2x / 12 taps on its own kernel, any other ratios and tap
+    counts on the general one)."""
 
     def __init__(self, activation, antialias: bool = False, up_ratio: int = 2, down_ratio: int = 2,
                  up_kernel_size: int = 12, down_kernel_size: int = 12):
@@ -230,9 +231,6 @@ class Activation1d(nn.Module):
         self.down_ratio = down_ratio
         self.act = activation
         if antialias:
-            if (up_ratio, down_ratio, up_kernel_size, down_kernel_size) != (2, 2, 12, 12):
-                raise NotImplementedError("anti-aliased Activation1d is implemented for ratio 2, 12 taps "
-                                          "(the only configuration the reference builds)")
             self.upsample = UpSample1d(up_ratio, up_kernel_size)
             self.downsample = DownSample1d(down_ratio, down_kernel_size)
         self._fcache = _DeviceCache()
@@ -257,7 +255,10 @@ class Activation1d(nn.Module):
         x = _as_input(x)
         a, ib = self.act.coeffs(x.device)
         fu, fd = self.filters(x.device)
-        return _ops().aa_snake(x, a, ib, fu, fd)
+        if (self.up_ratio, self.down_ratio, fu.numel(), fd.numel()) == (2, 2, 12, 12):
+            return _ops().aa_snake(x, a, ib, fu, fd)
+        # other constructor ratios / tap counts (act.py:8-23): the general kernel (bc_aa_snake_fwd_ex)
+        return _ops().aa_snake_ex(x, a, ib, fu, fd, self.up_ratio, self.down_ratio)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -24,7 +24,7 @@ _lock = threading.Lock()
 _ns = None
 
 # every op the extension defines (tests check the registry against this list)
-OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "tanh", "reslstm", "reslstm_bidir", "vq_prepare_codebook", "vq",
+OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "aa_snake_ex", "tanh", "reslstm", "reslstm_bidir", "vq_prepare_codebook", "vq",
        "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "resample_sinc", "synth_clips_")
 
 
@@ -75,6 +75,13 @@ def _register_fakes():
     @reg("bigcodec::aa_snake")
     def _aa(x, a, ib, fu, fd):
         return _new(x, x.shape)
+
+    @reg("bigcodec::aa_snake_ex")
+    def _aa_ex(x, a, ib, fu, fd, up_ratio, down_ratio):
+        kd = fd.numel()
+        L = x.shape[2] * up_ratio
+        n = L + (kd // 2 - (1 if kd % 2 == 0 else 0)) + kd // 2 - kd
+        return _new(x, (x.shape[0], x.shape[1], n // down_ratio + 1 if n >= 0 else 0))
 
     @reg("bigcodec::tanh")
     def _tanh(x):

@@ -114,6 +114,15 @@ int bc_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snak
 int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
                     const float* up_filter, const float* down_filter, float* y,
                     int B, int C, int T, void* stream);
+/* bc_aa_snake_fwd_ex: the same for Activation1d(up_ratio, down_ratio, up_kernel_size, down_kernel_size)
+ * (act.py:8-23; resample.py:10-33 geometry for any ratio): up_filter has up_taps floats, down_filter
+ * down_taps; ratios 1..16, taps up to 256 (up_taps >= up_ratio), else 3.  y: [B][C][Tout] with
+ * Tout = bc_aa_snake_out_len(T, up_ratio, down_ratio, down_taps) (= T when the ratios are equal and
+ * down_taps is even).  (2, 12, 2, 12) runs bc_aa_snake_fwd's kernel. */
+long long bc_aa_snake_out_len(int T, int up_ratio, int down_ratio, int down_taps);
+int bc_aa_snake_fwd_ex(const float* x, const float* snake_alpha_exp, const float* snake_inv_beta,
+                       const float* up_filter, const float* down_filter, float* y, int B, int C, int T, int up_ratio,
+                       int up_taps, int down_ratio, int down_taps, void* stream);
 
 /* Diagnostics (bench.py's roofline attribution, no compute): the kernel symbol a bc_conv1d_fwd launch with
  * this cfg (K = the conv's kernel size, before any phase decomposition) or a bc_resunit_fwd launch runs, as

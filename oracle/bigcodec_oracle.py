@@ -51,10 +51,10 @@ def snake_beta(x: Tensor, alpha: Tensor, beta: Tensor, logscale: bool = True) ->
     return x + (1.0 / (beta + 0.000000001)) * torch.pow(torch.sin(x * alpha), 2)
 
 
-def upsample2(x: Tensor, filt: Tensor) -> Tensor:
-    """UpSample1d(ratio=2, kernel 12).forward, vq/alias_free_torch/resample.py:25-33."""
+def upsample2(x: Tensor, filt: Tensor, ratio: int = 2) -> Tensor:
+    """UpSample1d(ratio, kernel).forward, vq/alias_free_torch/resample.py:10-33 (default ratio 2, 12 taps)."""
     C = x.shape[1]
-    ratio, k = 2, filt.shape[-1]
+    k = filt.shape[-1]
     pad = k // ratio - 1
     pad_left = pad * ratio + (k - ratio) // 2
     pad_right = pad * ratio + (k - ratio + 1) // 2
@@ -63,24 +63,24 @@ def upsample2(x: Tensor, filt: Tensor) -> Tensor:
     return x[..., pad_left:-pad_right]
 
 
-def downsample2(x: Tensor, filt: Tensor) -> Tensor:
-    """DownSample1d(ratio=2, kernel 12) -> LowPassFilter1d.forward, filter.py:86-95."""
+def downsample2(x: Tensor, filt: Tensor, ratio: int = 2) -> Tensor:
+    """DownSample1d(ratio, kernel) -> LowPassFilter1d.forward, resample.py:36-49, filter.py:86-95."""
     C = x.shape[1]
     k = filt.shape[-1]
     even = k % 2 == 0
     pad_left = k // 2 - int(even)
     pad_right = k // 2
     x = F.pad(x, (pad_left, pad_right), mode="replicate")
-    return F.conv1d(x, filt.expand(C, -1, -1), stride=2, groups=C)
+    return F.conv1d(x, filt.expand(C, -1, -1), stride=ratio, groups=C)
 
 
-def activation(x: Tensor, sd: SD, prefix: str, antialias: bool) -> Tensor:
+def activation(x: Tensor, sd: SD, prefix: str, antialias: bool, up_ratio: int = 2, down_ratio: int = 2) -> Tensor:
     """Activation1d(SnakeBeta).forward, vq/alias_free_torch/act.py:25-32."""
     if antialias:
-        x = upsample2(x, sd[prefix + "upsample.filter"])
+        x = upsample2(x, sd[prefix + "upsample.filter"], up_ratio)
     x = snake_beta(x, sd[prefix + "act.alpha"], sd[prefix + "act.beta"])
     if antialias:
-        x = downsample2(x, sd[prefix + "downsample.lowpass.filter"])
+        x = downsample2(x, sd[prefix + "downsample.lowpass.filter"], down_ratio)
     return x
 
 

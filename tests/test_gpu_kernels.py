@@ -162,6 +162,25 @@ def test_aa_activation(dev, golden):
         assert_close_rel(got, torch.from_numpy(gd[f"y_{T}"]), 2e-6, f"aa T={T}")
 
 
+def test_aa_activation_ratios(dev, golden):
+    """Activation1d with non-default up / down ratios and tap counts (bc_aa_snake_fwd_ex's general
+    kernel) against the reference's outputs (tests/golden/aa_activation_ratios.npz)."""
+    gd = golden("aa_activation_ratios.npz")
+    meta = gd["meta"]
+    for ci, (ru, rd, ku, kd) in enumerate(meta["cases"]):
+        for T in meta["T"]:
+            k = f"c{ci}_T{T}"
+            act = M.Activation1d(M.SnakeBeta(5, alpha_logscale=True), antialias=True, up_ratio=ru, down_ratio=rd,
+                                 up_kernel_size=ku, down_kernel_size=kd)
+            with torch.no_grad():
+                act.act.alpha.copy_(torch.from_numpy(gd[f"alpha_{k}"]))
+                act.act.beta.copy_(torch.from_numpy(gd[f"beta_{k}"]))
+            want = torch.from_numpy(gd[f"y_{k}"])
+            got = act.to(dev)(torch.from_numpy(gd[f"x_{k}"]).to(dev)).cpu()
+            assert got.shape == want.shape, (k, got.shape, want.shape)
+            assert_close_rel(got, want, 2e-6, f"aa ratios {(ru, rd, ku, kd)} T={T}")
+
+
 @pytest.mark.parametrize("H,layers,B,T", [(64, 2, 3, 50), (512, 1, 2, 20), (128, 2, 70, 9), (1536, 2, 2, 6),
                                           (256, 2, 130, 7), (512, 2, 64, 40), (1536, 1, 64, 25)])
 def test_reslstm(dev, H, layers, B, T, prec):

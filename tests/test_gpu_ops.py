@@ -48,6 +48,11 @@ def _cases(dev, base):
     (wih, whh, lb), _ = lstm.lstm.prepared(dev)
     xl = torch.randn(2, H, 9, generator=g).to(dev)
     cases.append(("reslstm", (xl, wih, lb, whh, None, None, L.precision_mode(), None, None, True)))
+    from audiotokenization_amd import modules as M
+
+    act = M.Activation1d(M.SnakeBeta(C, alpha_logscale=True), antialias=True, up_ratio=3, down_ratio=2).to(dev)
+    fu, fd = act.filters(dev)
+    cases.append(("aa_snake_ex", (x, a, ib, fu, fd, 3, 2)))
     bl = ResLSTM(64, num_layers=1, bidirectional=True).to(dev)
     (bwih, bwhh, bb), _ = bl.lstm.prepared(dev)
     cases.append(("reslstm_bidir", (torch.randn(2, 64, 7, generator=g).to(dev), bwih, bb, bwhh, None, None,

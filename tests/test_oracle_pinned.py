@@ -68,6 +68,25 @@ def test_aa_fixture(golden):
         assert torch.equal(y, torch.from_numpy(g[f"y_{T}"])), T
 
 
+def test_aa_ratios_fixture(golden):
+    """Non-default Activation1d ratios / tap counts (act.py:8-23) against the reference's own outputs
+    (tools/make_golden_aa_ratios.py): the product's filter buffers and the oracle restatement."""
+    from audiotokenization_amd.modules import DownSample1d, UpSample1d
+
+    g = golden("aa_activation_ratios.npz")
+    meta = g["meta"]
+    for ci, (ru, rd, ku, kd) in enumerate(meta["cases"]):
+        up, dn = UpSample1d(ru, ku), DownSample1d(rd, kd)
+        assert np.array_equal(up.filter.numpy(), g[f"up_filter_c{ci}"]), ci
+        assert np.array_equal(dn.lowpass.filter.numpy(), g[f"down_filter_c{ci}"]), ci
+        for T in meta["T"]:
+            k = f"c{ci}_T{T}"
+            sd = {"act.alpha": torch.from_numpy(g[f"alpha_{k}"]), "act.beta": torch.from_numpy(g[f"beta_{k}"]),
+                  "upsample.filter": up.filter, "downsample.lowpass.filter": dn.lowpass.filter}
+            y = O.activation(torch.from_numpy(g[f"x_{k}"]), sd, "", True, ru, rd)
+            assert torch.equal(y, torch.from_numpy(g[f"y_{k}"])), k
+
+
 def test_vq_fixture_torch_oracle(golden):
     g = golden("vq_decode_latents.npz")
     z = torch.from_numpy(g["z_e"])
