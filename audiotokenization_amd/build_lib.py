@@ -62,14 +62,32 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 return LIB
     hipcc = _hipcc()
 
+    common = hashlib.sha256()  # every header (any source may include any of them) + the flags
+    for f in HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            common.update(fh.read())
+    with open(os.path.join(REPO, "include", "bigcodec.h"), "rb") as fh:
+        common.update(fh.read())
+    common.update(" ".join(CFLAGS).encode())
+
     def compile_one(src: str) -> str:
         obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        h = common.copy()
+        with open(os.path.join(CSRC, src), "rb") as fh:
+            h.update(fh.read())
+        ostamp = obj + ".stamp"
+        if not force and os.path.exists(obj) and os.path.exists(ostamp):
+            with open(ostamp) as fh:
+                if fh.read().strip() == h.hexdigest():
+                    return obj  # unchanged source and headers: keep the object
         cmd = [hipcc, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{res.stderr}")
+        with open(ostamp, "w") as fh:
+            fh.write(h.hexdigest())
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8, 16)) as ex:

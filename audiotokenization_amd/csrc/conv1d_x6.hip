@@ -125,24 +125,40 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 //   stride >= 3, d = 1, Cout % 192 == 0 -> phase-decomposed 120 (two taps per K-step fit, 121 runs
 //                                     one): the stride-5 downsampling 384 -> 768 / 768 -> 1536 -3 / -7 %
 //                                     vs phase-decomposed 121 (profiles/r02_s2_sweep.txt)
+// The 16-wave (1024-thread) 192 x 256 tile 122 (96 x 32 per wave) by shape class, a bit each
+// (BC_X6_W16 overrides the mask for A/B timing):
+//   1: stride-1 multi-tap convs with Cout % 192 == 0 instead of the 8-wave 120
+//   2: the phase-decomposed strided convs with Cout % 192 == 0 instead of 120
+//   4: the k7 C = 768 convs instead of the 256 x 256 tile 121
+//   8: the pointwise C = 192 convs instead of 114
+static int x6_w16() {
+  static const int v = [] {
+    const char* e = getenv("BC_X6_W16");
+    return e ? atoi(e) : 15;
+  }();
+  return v;
+}
+static int w16(int bit, int tile8, int tile16) { return (x6_w16() & bit) ? tile16 : tile8; }
+
 static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
   if (s == 1 && K == 1) {
     if (Cout >= 2048 && Cout % 256 == 0) return 121;
-    if (Cout % 192 == 0) return 114;
+    if (Cout % 192 == 0) return Cout == 192 ? w16(8, 114, 122) : 114;
   }
   if (s == 1 && K > 1) {
     const bool f320 = Cout % 192 == 0, f321 = Cout % 256 == 0;
     auto fits = [&](int tile) { return x6_ncol(kX6Tiles[tile], K, 1, d) <= 32 * X6_MAXCOL_ITERS; };
+    if (Cout == 768 && (x6_w16() & 4) && fits(22)) return 122;
     if ((Cout == 768 || (f321 && !f320)) && fits(21)) return 121;
-    if (f320 && fits(20)) return 120;
+    if (f320 && fits(20)) return w16(1, 120, 122);
   }
   auto phase_fits = [&](int tile) {
     return x6_ncol(kX6Tiles[tile], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS;
   };
-  if (s == 2 && d == 1 && Cout % 384 == 0 && phase_fits(20)) return 2000 + 120;
+  if (s == 2 && d == 1 && Cout % 384 == 0 && phase_fits(20)) return 2000 + w16(2, 120, 122);
   if (s == 2 && d == 1 && Cout % 192 == 0 && Cout <= 384) return 115;
-  if (s >= 3 && s <= 16 && d == 1 && Cout % 192 == 0 && phase_fits(20)) return 1000 * s + 120;
+  if (s >= 3 && s <= 16 && d == 1 && Cout % 192 == 0 && phase_fits(20)) return 1000 * s + w16(2, 120, 122);
   if (s >= 3 && s <= 16 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[21], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS)
     return 1000 * s + 121;
   if (s >= 3 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[2], K, s, d) <= 32 * X6_MAXCOL_ITERS) return 102;
@@ -152,7 +168,8 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
   if (planes <= 2 && x6_occ_pref() == 0) {  // bf16 (1 plane) follows the h3 table (measured, config 5)
-    const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
+    int c = h3_preferred_cfg(Cout, Cin, K, s, d);
+    if (planes == 1 && c % 1000 == 122) c -= 2;  // the 16-wave tile is compiled for h3 only: bf16 keeps 120
     if (c >= 0) return c + (planes == 2 ? 200 : 100);  // (a phase-decomposed 1000 * s + tile keeps its phase factor)
   }
   if (planes >= 2 && x6_occ_pref() == 0) {

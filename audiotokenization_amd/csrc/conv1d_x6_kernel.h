@@ -45,14 +45,18 @@ namespace bc {
 // LDS writes overlap the other waves' MFMAs.
 template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
-// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.
-__global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvArgs a) {
+// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.  WM * WN = 16: one
+// 1024-thread workgroup (four waves per SIMD, <= 128 VGPRs).
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 4 : 2))) conv1d_x6_kernel(ConvArgs a) {
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
-  constexpr int CI = PW ? BN / 32 : X6_MAXCOL_ITERS;  // 32-column B passes per chunk
+  constexpr int NW = WM * WN;  // waves: 8 or 16
+  static_assert(NW == 8 || NW == 16, "512- or 1024-thread workgroups");
+  constexpr int NCG = NW / 8;  // B staging column groups (16 channel pairs x 32 column lanes each)
+  constexpr int CI = ((PW ? BN / 32 : X6_MAXCOL_ITERS) + NCG - 1) / NCG;  // 32-column B passes per thread
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
-  __shared__ unsigned smax[2][8];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
+  __shared__ unsigned smax[2][NW];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
   typedef typename FragType<P>::type frag_t;
 
   const int ncol = a.win;                // columns of the input tile
@@ -101,14 +105,16 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     const int n = (K - t0 < TPS ? K - t0 : TPS) * a_pieces;
     const unsigned char* src = wblk + (long long)(c * K + t0) * (a_pieces * 1024);
     unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
-    for (int q = wave; q < n; q += 8)
+    for (int q = wave; q < n; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);
   };
 
-  // B staging: thread -> (channel pair p, column lane cl); columns cl + 32*i, i < CI
-  const int bp = tid >> 5;       // 0..15
+  // B staging: thread -> (channel pair p, column lane cl, column group g); columns cl + 32 * (i * NCG + g)
+  const int bp = (tid >> 5) & 15;
   const int bcl = tid & 31;
+  const int bcg = tid >> 9;  // 0 with 8 waves
+  auto bcol = [&](int i) { return bcl + 32 * (i * NCG + bcg); };
   float bv0[CI], bv1[CI];
   auto load_b = [&](int chunk, float (&v0)[CI], float (&v1)[CI]) {
     const int ci0 = chunk * X6_BKC + 2 * bp;
@@ -123,7 +129,7 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
     }
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
+      const int col = bcol(i);
       const int t0 = tb0 + col * tstep, t1 = tb1 + col * tstep;
       const bool cin = col < ncol;
       const unsigned o0 = (cin && ci0 < a.Cin && t0 >= 0 && t0 < a.Tin) ? (unsigned)((ch0 * a.Tin + t0) * 4) : 0xfffffff0u;
@@ -148,14 +154,14 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) conv1d_x6_kernel(ConvA
   auto bmax_scale = [&](int par) {
     unsigned m = smax[par][0];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) m = m > smax[par][w] ? m : smax[par][w];
+    for (int w = 1; w < NW; ++w) m = m > smax[par][w] ? m : smax[par][w];
     return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
   };
   float xs = 1.f;  // P == 2: scale of the staged chunk and of the accumulator
   auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI], unsigned char* Bt, float sc) {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
+      const int col = bcol(i);
       if (col < ncol) {
         const float v0 = w0[i], v1 = w1[i];
         if constexpr (P == 2) {
@@ -400,6 +406,7 @@ inline constexpr X6Tile kX6Tiles[] = {
     {4, 4, 4, 2},  // 119: BM=256 BN=128
     {6, 4, 2, 4},  // 120: BM=192 BN=256  (h3: 96 x 64 per wave)
     {8, 4, 2, 4},  // 121: BM=256 BN=256
+    {6, 2, 2, 8},  // 122: BM=192 BN=256, 16 waves of 96 x 32 (h3 only)
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -464,7 +471,7 @@ inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
 
 template <int MT, int NT, int WM, int WN, int P>
 static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
-  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, NTHR = 64 * WM * WN;
   const X6Tile t{MT, NT, WM, WN};
   const int ncol = x6_ncol(t, a.K, a.s, a.d);
   if (ncol > 32 * X6_MAXCOL_ITERS) return BC_ERR_UNSUPPORTED;
@@ -488,17 +495,30 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   constexpr int T2 = P <= 2 ? 2 : 1;
   constexpr bool D2 = P <= 2;
   if (v.pw)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(512), v.lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   else if (v.db && v.tps == 2)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2, D2>), dim3(a.nwg), dim3(512), v.lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2, D2>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   else if (v.db)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 1, D2>), dim3(a.nwg), dim3(512), v.lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 1, D2>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   else if (v.tps == 2)
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2>), dim3(a.nwg), dim3(512), v.lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T2>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   else
-    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(512), v.lds, st, a);
+    hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   BC_CHECK_LAUNCH();
   return BC_OK;
+}
+
+// the 16-wave tile (h3 only: no x6 / bf16 instances are compiled).  Measured and not kept
+// (profiles/r02g_w16_tiles.txt, r02g_w16b.txt): 48 x 64 per wave (111 spilled VGPRs, 2.5x slower) and a
+// 256 x 256 tile of 128 x 32 per wave (86-136 spilled VGPRs, 2.2-2.6x slower).
+template <int P>
+static int launch_x6_w16(ConvArgs& a, int B, hipStream_t st) {
+  if constexpr (P == 2) {
+    return launch_x6<6, 2, 2, 8, P>(a, B, st);
+  } else {
+    (void)a, (void)B, (void)st;
+    return BC_ERR_UNSUPPORTED;
+  }
 }
 
 // launch tile index `tile` (kX6Tiles) with P operand planes; instantiated in conv1d_x6_p<P>.hip
@@ -529,6 +549,7 @@ int x6_launch_tile(ConvArgs& a, int B, int tile, hipStream_t st);
     case 19: return launch_x6<4, 4, 4, 2, P>(a, B, st);            \
     case 20: return launch_x6<6, 4, 2, 4, P>(a, B, st);            \
     case 21: return launch_x6<8, 4, 2, 4, P>(a, B, st);            \
+    case 22: return launch_x6_w16<P>(a, B, st);                    \
   }                                                                \
   return BC_ERR_ARG;
 

@@ -89,6 +89,45 @@ def test_conv1d(dev, case, prec):
         assert_close_rel(got.cpu(), want, tol, f"conv {case}")
 
 
+@pytest.mark.parametrize("Cin,Cout,K,s,d,T,cfgs", [
+    (192, 192, 7, 1, 9, 700, (320, 322)), (384, 384, 7, 1, 3, 515, (320, 322)), (192, 192, 7, 1, 1, 256, (320, 322)),
+    (768, 768, 7, 1, 9, 300, (320, 322)), (384, 768, 10, 5, 1, 300, (5320, 5322)),
+    (192, 384, 4, 2, 1, 520, (2320, 2322)), (768, 1536, 10, 5, 1, 130, (5320, 5322))])
+def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs):
+    """The 192 x 256 h3 tile with 8 waves of 96 x 64 (cfg 320) and with 16 waves of 96 x 32 (322; the
+    phase-decomposed strided convs as 1000 s + tile) stages the same B chunks with the same block scales
+    and runs the same per-output MFMA chains: bit-identical outputs, and within the conv tolerance of the
+    oracle."""
+    old = L.precision_mode()
+    L.set_precision("h3")
+    try:
+        g = torch.Generator().manual_seed(Cin * 31 + Cout + d)
+        pad = K // 2 * d if s == 1 else s // 2 + s % 2
+        m = CV.WNConv1d(Cin, Cout, kernel_size=K, stride=s, dilation=d, padding=pad)
+        conv = _rand_wn_conv(m, g)
+        B = 2
+        x = torch.randn(B, Cin, T, generator=g)
+        sd = {k: v.detach() for k, v in conv.state_dict().items()}
+        want = O.conv(x, sd, "", K, s, pad, d, False)
+        Tout = want.shape[-1]
+        m.to(dev)
+        xd = x.to(dev)
+        st = torch.cuda.current_stream().cuda_stream
+        outs = {}
+        for cfg in cfgs:
+            wp, bias = m.packed_as(cfg, dev)
+            y = torch.empty(B, Cout, Tout, device=dev)
+            L.call("bc_conv1d_fwd", xd.data_ptr(), wp.data_ptr(), L.ptr(bias), 0, 0, 0, y.data_ptr(), 0,
+                   B, Cin, T, Cout, Tout, K, s, d, pad, 0, cfg, st)
+            torch.cuda.synchronize()
+            outs[cfg] = y.cpu()
+        assert_close_rel(outs[cfgs[0]], want, 3e-6 * max(1.0, np.sqrt(Cin * K / 64)), f"h3 {cfgs[0]}")
+        for c in cfgs[1:]:
+            assert torch.equal(outs[c], outs[cfgs[0]]), (c, (outs[c] - outs[cfgs[0]]).abs().max())
+    finally:
+        L._mode = old
+
+
 CONVT_CASES = [
     # Cin, Cout, stride, causal, snake, B, T
     (64, 32, 2, False, True, 2, 301),
