@@ -131,10 +131,11 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 //   2: the phase-decomposed strided convs with Cout % 192 == 0 instead of 120
 //   4: the k7 C = 768 convs instead of the 256 x 256 tile 121
 //   8: the pointwise C = 192 convs instead of 114
+//  16: the pointwise Cout >= 2048 convs (the LSTM input projection) instead of the 256 x 256 tile 121
 static int x6_w16() {
   static const int v = [] {
     const char* e = getenv("BC_X6_W16");
-    return e ? atoi(e) : 15;
+    return e ? atoi(e) : 31;
   }();
   return v;
 }
@@ -143,6 +144,7 @@ static int w16(int bit, int tile8, int tile16) { return (x6_w16() & bit) ? tile1
 static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
   if (s == 1 && K == 1) {
+    if (Cout >= 2048 && Cout % 192 == 0 && (x6_w16() & 16)) return 122;
     if (Cout >= 2048 && Cout % 256 == 0) return 121;
     if (Cout % 192 == 0) return Cout == 192 ? w16(8, 114, 122) : 114;
   }
@@ -168,8 +170,7 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
   if (planes <= 2 && x6_occ_pref() == 0) {  // bf16 (1 plane) follows the h3 table (measured, config 5)
-    int c = h3_preferred_cfg(Cout, Cin, K, s, d);
-    if (planes == 1 && c % 1000 == 122) c -= 2;  // the 16-wave tile is compiled for h3 only: bf16 keeps 120
+    const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
     if (c >= 0) return c + (planes == 2 ? 200 : 100);  // (a phase-decomposed 1000 * s + tile keeps its phase factor)
   }
   if (planes >= 2 && x6_occ_pref() == 0) {

@@ -406,7 +406,7 @@ inline constexpr X6Tile kX6Tiles[] = {
     {4, 4, 4, 2},  // 119: BM=256 BN=128
     {6, 4, 2, 4},  // 120: BM=192 BN=256  (h3: 96 x 64 per wave)
     {8, 4, 2, 4},  // 121: BM=256 BN=256
-    {6, 2, 2, 8},  // 122: BM=192 BN=256, 16 waves of 96 x 32 (h3 only)
+    {6, 2, 2, 8},  // 122: BM=192 BN=256, 16 waves of 96 x 32 (h3 and bf16)
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -508,12 +508,12 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   return BC_OK;
 }
 
-// the 16-wave tile (h3 only: no x6 / bf16 instances are compiled).  Measured and not kept
+// the 16-wave tile (h3 and bf16; the x6 planes do not fit its 128 VGPRs, so no x6 instances are compiled).  Measured and not kept
 // (profiles/r02g_w16_tiles.txt, r02g_w16b.txt): 48 x 64 per wave (111 spilled VGPRs, 2.5x slower) and a
 // 256 x 256 tile of 128 x 32 per wave (86-136 spilled VGPRs, 2.2-2.6x slower).
 template <int P>
 static int launch_x6_w16(ConvArgs& a, int B, hipStream_t st) {
-  if constexpr (P == 2) {
+  if constexpr (P <= 2) {
     return launch_x6<6, 2, 2, 8, P>(a, B, st);
   } else {
     (void)a, (void)B, (void)st;

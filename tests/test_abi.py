@@ -262,7 +262,10 @@ def test_kernel_names_come_from_the_launchers():
             mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
             assert name == f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>", name
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false>")  # pointwise
-    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3).endswith("false, 1, true>")
+    # k7 C = 768: the 16-wave 192 x 256 tile, two taps per K-step; the final k3 keeps the double-buffered 256 x 256
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3) == \
+        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>"
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 3), 3).endswith("false, 1, true>")
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_rr_kernel<48, 4, 1>"
     n96 = L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 3), 96, 3)
     assert n96.startswith("resunit_x6_kernel<") and ", 2, " in n96, n96
