@@ -159,6 +159,9 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
     return x6_ncol(kX6Tiles[tile], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS;
   };
   if (s == 2 && d == 1 && Cout % 384 == 0 && phase_fits(20)) return 2000 + w16(2, 120, 122);
+  // 96 -> 192: 3.39 -> 2.69 ms on the phase-decomposed 16-wave tile (profiles/r02h_s2_w16.txt; 48 -> 96, a
+  // half-empty 192-row tile, stays on 109)
+  if (s == 2 && d == 1 && Cout % 192 == 0 && (x6_w16() & 2) && phase_fits(22)) return 2000 + 122;
   if (s == 2 && d == 1 && Cout % 192 == 0 && Cout <= 384) return 115;
   if (s >= 3 && s <= 16 && d == 1 && Cout % 192 == 0 && phase_fits(20)) return 1000 * s + w16(2, 120, 122);
   if (s >= 3 && s <= 16 && d == 1 && Cout % 256 == 0 && x6_ncol(kX6Tiles[21], (K + s - 1) / s, 1, 1) <= 32 * X6_MAXCOL_ITERS)

@@ -92,7 +92,8 @@ def test_conv1d(dev, case, prec):
 @pytest.mark.parametrize("Cin,Cout,K,s,d,T,cfgs", [
     (192, 192, 7, 1, 9, 700, (320, 322)), (384, 384, 7, 1, 3, 515, (320, 322)), (192, 192, 7, 1, 1, 256, (320, 322)),
     (768, 768, 7, 1, 9, 300, (320, 322)), (384, 768, 10, 5, 1, 300, (5320, 5322)),
-    (192, 384, 4, 2, 1, 520, (2320, 2322)), (768, 1536, 10, 5, 1, 130, (5320, 5322))])
+    (192, 384, 4, 2, 1, 520, (2320, 2322)), (96, 192, 4, 2, 1, 600, (2320, 2322)),
+    (768, 1536, 10, 5, 1, 130, (5320, 5322))])
 @pytest.mark.parametrize("tprec", ["h3", "bf16"])
 def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
     """The 192 x 256 h3 tile with 8 waves of 96 x 64 (cfg 320) and with 16 waves of 96 x 32 (322; the
