@@ -1,3 +1,5 @@
+# Historical (profiles/r02g_w16*.txt): cfg 322 / 323 / 324 here are the tile table of commit 3dcd5a4; only the
+# 96 x 32-per-wave 16-wave tile was kept, and it is cfg 322 now (kX6Tiles index 22).
 # 192 x 256 k7 tile: 8 waves (cfg 320) vs 16 waves (322: 48 x 64 per wave, 323: 96 x 32 per wave), h3.
 set -u
 mkdir -p gpurun_out

@@ -1,3 +1,5 @@
+# Historical (profiles/r02g_w16*.txt): cfg 322 / 323 / 324 here are the tile table of commit 3dcd5a4; only the
+# 96 x 32-per-wave 16-wave tile was kept, and it is cfg 322 now (kX6Tiles index 22).
 # 16-wave tiles, round 2: correctness of every 8- vs 16-wave pair, per-shape timing of the remaining
 # tile classes, the A-prefetch on / off question for tile 123 (exp/noapf.so: the same tree built with
 # APF off for 16-wave tiles), and the config-2 step under each BC_X6_W16 mask.

@@ -1,3 +1,5 @@
+# Historical (profiles/r02g_w16*.txt): cfg 322 / 323 / 324 here are the tile table of commit 3dcd5a4; only the
+# 96 x 32-per-wave 16-wave tile was kept, and it is cfg 322 now (kX6Tiles index 22).
 # 16-wave tile 122: correctness (every 8- vs 16-wave pair, the conv cases) and the config-2 step under
 # BC_X6_W16 masks 3 (default: k7 + strided), 7 (+ k7 C = 768), 11 (+ pointwise C = 192).
 set -u
