@@ -5,6 +5,7 @@ missing or fails to load, every op raises immediately (BigCodecLibraryError).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -118,6 +119,21 @@ def defer_status(status, what: str) -> None:
     """Remember a device status word (nonzero = the launch failed, e.g. a persistent-kernel timeout,
     include/bigcodec.h) to be checked by check_status() before the caller's output is consumed."""
     _pending_status.append((status, what))
+
+
+@contextlib.contextmanager
+def status_scope():
+    """Scope the deferred status words to one top-level forward: the body's launches defer into a fresh
+    list, the body ends with check_status(); when the body raises instead, its unchecked words are dropped
+    with it (that forward's output is never consumed), so a later forward cannot raise for a batch that
+    already failed (a stale status after a per-batch error in the extraction loops).  Scopes
+    nest: the enclosing forward's words are restored on exit."""
+    global _pending_status
+    outer, _pending_status = _pending_status, []
+    try:
+        yield
+    finally:
+        _pending_status = outer
 
 
 def check_status() -> None:

@@ -332,6 +332,7 @@ class ResLSTM(nn.Module):
         return y, next_act(y)
 
     def forward(self, x):
-        y = self.run(x)
-        L.check_status()
+        with L.status_scope():
+            y = self.run(x)
+            L.check_status()
         return y

@@ -51,6 +51,10 @@ class BigCodecEncoder(nn.Module):
         self.enc_dim = d_model
 
     def forward(self, x):
+        with L.status_scope():
+            return self._forward(x)
+
+    def _forward(self, x):
         x = _as_input(x)
         blk = list(self.block)
         final_act, last_conv = blk[-2], blk[-1]
@@ -123,6 +127,10 @@ class BigCodecDecoder(nn.Module):
     def decode(self, x):
         """self.model(x): fused flow; final Snake in the producer of the last conv's input, tanh in
         the last conv's epilogue."""
+        with L.status_scope():
+            return self._decode(x)
+
+    def _decode(self, x):
         x = _as_input(x)
         m = list(self.model)
         final_act, last_conv = m[-3], m[-2]

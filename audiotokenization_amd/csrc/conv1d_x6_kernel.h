@@ -303,6 +303,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     if (a.nchunks > 1) load_b(1, bw0, bw1);
     auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
       if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
+      dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
       if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) load_b(c + 2, p0v, p1v);
       compute(c & 1, 0, 0);
       if (c + 1 < a.nchunks) {
@@ -331,7 +332,10 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       for (int tp = 0; tp < kst; ++tp) {
         const int step = c * kst + tp;
         if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
-        if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) load_b(c + 1, bv0, bv1);
+        if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) {
+          dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
+          load_b(c + 1, bv0, bv1);
+        }
         if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int tt = 0; tt < TPS; ++tt) {

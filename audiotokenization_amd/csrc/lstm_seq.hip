@@ -21,11 +21,15 @@
 //   fragment-native sequence buffer hseq[t][k-step][n-tile][plane][lane][8 bf16] (the consumers'
 //   MFMA B fragments as they are), drains them (vmcnt(0)) and one lane stores flags[g] = t+1
 //   (relaxed, agent scope).  Consumer wave w polls the flags of the G/4 workgroups that produce its
-//   K range (sc1 loads, bounded spin), then reads slot t-1 with PLAIN loads: every slot is written
-//   once per launch and read only after its flag, so no L1/L2 of this launch can hold an older
-//   copy of those lines (kernel boundaries invalidate the caches), and the first CU of an XCD to
-//   miss pulls the line into that XCD's L2 for the other 23.  (Measured: sc1 loads of a reused
-//   double buffer instead — every CU fetching its 393 KB over the fabric — cost 11.6 us per step.)
+//   K range (sc1 loads, bounded spin), then reads slot t-1 with 16-byte sc1 buffer loads
+//   (ls_load_sc1).  That is the measured-valid hand-off of MI355X_MICROARCH.md (§Workgroup dispatch,
+//   "Valid forms", table row 1: sc1 payload stores, vmcnt(0), one lane's sc1 flag store; sc1 poll;
+//   EVERY load of the handed-off bytes an sc1 load).  Rounds 1-2 read the slot with PLAIN loads and
+//   no agent-scope acquire, arguing that a slot written once per launch cannot be cached stale; the
+//   guide lists exactly that form as invalid ("no acquire -> stale, first touch included"), and
+//   it is the one cross-workgroup hand-off of the x6 full-size path whose visibility was not
+//   guaranteed (x6 latent 5.1e-4 off on one box).  sc1 loads bypass
+//   only the CU's L1; the XCD's L2 still serves its CUs.
 //   Every poll is bounded: on timeout the kernel counts it in *status and all workgroups leave.
 #include <algorithm>
 #include <cmath>
@@ -115,6 +119,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ls_rsrc(const void* p, unsigne
                                            __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// 16-byte sc1 load of a handed-off h_t fragment (L1 bypass: see the hand-off notes at the top)
+template <typename T>
+__device__ __forceinline__ T ls_load_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  static_assert(sizeof(T) == 16, "16-byte fragments");
+  return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LS_SC1));
+}
+
 template <int KS>
 __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
   __shared__ floatx4 red[LS_WAVES][8][64];  // per-wave partial gates of the 8 (m-tile, n-tile) tiles
@@ -202,22 +213,23 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the poll
+      // compiler ordering only (keeps the loads below the poll); visibility comes from the sc1 loads
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       LS_STAMP(1)
-      // h_{t-1} lives at addresses no cache of this launch has seen before it was written through
-      // (one slot per step), so plain L2-cached loads are fresh and the XCD's L2 serves its CUs.
+      // h_{t-1}: sc1 loads of slot t-1 (the hand-off form at the top of the file).
       // h arrives already split into its three bf16 planes (the producer splits once), as MFMA B
       // fragments: 3 x 16 B per lane per (k-step, n-tile).  Register double buffer: the 12 loads of
       // k-step ks+1 are in flight while k-step ks runs its 48 MFMAs (one wave per SIMD: nothing else
       // hides the L2 latency).
-      const ls_bf16x8* hp = reinterpret_cast<const ls_bf16x8*>(a.hseq + (long long)(t - 1) * hstep) + lane;
+      const __amdgpu_buffer_rsrc_t hr = ls_rsrc(a.hseq + (long long)(t - 1) * hstep, (unsigned)(hstep * 4));
       ls_bf16x8 hbuf[2][4][3];
       auto load_ks = [&](int ks, ls_bf16x8 (&dst)[4][3]) {
         const int ksa = w * KS + ks;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-          for (int p = 0; p < 3; ++p) dst[nt][p] = hp[((ksa * 4 + nt) * 3 + p) * 64];
+          for (int p = 0; p < 3; ++p)
+            dst[nt][p] = ls_load_sc1<ls_bf16x8>(hr, (unsigned)((((ksa * 4 + nt) * 3 + p) * 64 + lane) * 16));
       };
       load_ks(0, hbuf[0]);
 #pragma unroll
@@ -463,10 +475,12 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        // compiler ordering only (keeps the loads below the poll); visibility comes from the sc1 loads
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         LS2_STAMP(1)
-        const frag_t* hp =
-            reinterpret_cast<const frag_t*>(a.hseq + ((long long)(t - 1 + sh) * 2 + h) * hhalf) + lane;
+        // h_{t-1} of this half: sc1 loads (the hand-off form at the top of the file)
+        const __amdgpu_buffer_rsrc_t hr = ls_rsrc(a.hseq + ((long long)(t - 1 + sh) * 2 + h) * hhalf,
+                                                  (unsigned)(hhalf * 4));
         // h_{t-1} fragments through a register ring LS_HD k-steps deep: the loads of k-step ks + LS_HD - 1
         // are issued before k-step ks's MFMAs, so L2 latency hides behind LS_HD - 1 k-steps of MFMAs
         // (depth 2 left ~2300 of a half-step's 4600 load+MFMA cycles exposed, profiles/r01g_lstm_h3_stamps.txt)
@@ -477,7 +491,8 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int p = 0; p < P; ++p) dst[nt][p] = hp[((ksa * 2 + nt) * P + p) * 64];
+            for (int p = 0; p < P; ++p)
+              dst[nt][p] = ls_load_sc1<frag_t>(hr, (unsigned)((((ksa * 2 + nt) * P + p) * 64 + lane) * 16));
         };
 #pragma unroll
         for (int ks = 0; ks + 1 < HD; ++ks) load_ks(ks, hbuf[ks]);

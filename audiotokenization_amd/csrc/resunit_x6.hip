@@ -217,7 +217,10 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
     for (int tp = 0; tp < kst; ++tp) {
       const int step = c * kst + tp;
       if (step + 1 < nsteps && !BC_ABL(r.dbg, 1)) issue_a(a.w, step + 1, (step + 1) & 1);
-      if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(r.dbg, 2)) load_b(c + 1);
+      if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(r.dbg, 2)) {
+        dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
+        load_b(c + 1);
+      }
 #pragma unroll
       for (int tt = 0; tt < TPS; ++tt) {
       const int tap = tp * TPS + tt;

@@ -11,6 +11,7 @@
 //
 // Reference call chains replaced: see include/bigcodec.h, one comment per entry point.
 #include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -416,6 +417,19 @@ void synth_clips_(const Tensor& x, int64_t clip0) {
   ok(bc_synth_clips(x.data_ptr<float>(), i32(B, "B"), T, clip0, stream_of(x)), "bc_synth_clips");
 }
 
+// Every op runs under a device guard of its first tensor argument (the data tensor), so the C ABI's launches
+// and the op's allocations land on that tensor's device even when it is not the current one (the ABI launches
+// on the current HIP device; c10 reports these tensors as "cuda", hence the masquerading guard).
+template <auto F>
+struct Guarded;
+template <typename R, typename First, typename... Rest, R (*F)(First, Rest...)>
+struct Guarded<F> {
+  static R call(First first, Rest... rest) {
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(first.device());
+    return F(first, rest...);
+  }
+};
+
 }  // namespace
 
 TORCH_LIBRARY(bigcodec, m) {
@@ -450,23 +464,23 @@ TORCH_LIBRARY(bigcodec, m) {
 }
 
 TORCH_LIBRARY_IMPL(bigcodec, CUDA, m) {
-  m.impl("conv1d", &conv1d);
-  m.impl("conv_transpose1d", &conv_transpose1d);
-  m.impl("resunit", &resunit);
-  m.impl("snake", &snake);
-  m.impl("aa_snake", &aa_snake);
-  m.impl("tanh", &tanh_op);
-  m.impl("aa_snake_ex", &aa_snake_ex);
-  m.impl("reslstm", &reslstm);
-  m.impl("reslstm_bidir", &reslstm_bidir);
-  m.impl("vq_prepare_codebook", &vq_prepare_codebook);
-  m.impl("vq", &vq);
-  m.impl("vq_argmin", &vq_argmin);
-  m.impl("vq2emb", &vq2emb);
-  m.impl("vq2emb_add_", &vq2emb_add_);
-  m.impl("rvq_update_", &rvq_update_);
-  m.impl("vq2emb_ct", &vq2emb_ct);
-  m.impl("fsq", &fsq);
-  m.impl("resample_sinc", &resample_sinc);
-  m.impl("synth_clips_", &synth_clips_);
+  m.impl("conv1d", &Guarded<&conv1d>::call);
+  m.impl("conv_transpose1d", &Guarded<&conv_transpose1d>::call);
+  m.impl("resunit", &Guarded<&resunit>::call);
+  m.impl("snake", &Guarded<&snake>::call);
+  m.impl("aa_snake", &Guarded<&aa_snake>::call);
+  m.impl("tanh", &Guarded<&tanh_op>::call);
+  m.impl("aa_snake_ex", &Guarded<&aa_snake_ex>::call);
+  m.impl("reslstm", &Guarded<&reslstm>::call);
+  m.impl("reslstm_bidir", &Guarded<&reslstm_bidir>::call);
+  m.impl("vq_prepare_codebook", &Guarded<&vq_prepare_codebook>::call);
+  m.impl("vq", &Guarded<&vq>::call);
+  m.impl("vq_argmin", &Guarded<&vq_argmin>::call);
+  m.impl("vq2emb", &Guarded<&vq2emb>::call);
+  m.impl("vq2emb_add_", &Guarded<&vq2emb_add_>::call);
+  m.impl("rvq_update_", &Guarded<&rvq_update_>::call);
+  m.impl("vq2emb_ct", &Guarded<&vq2emb_ct>::call);
+  m.impl("fsq", &Guarded<&fsq>::call);
+  m.impl("resample_sinc", &Guarded<&resample_sinc>::call);
+  m.impl("synth_clips_", &Guarded<&synth_clips_>::call);
 }

@@ -31,6 +31,16 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// Issue-order pin between an LDS-DMA copy (global_load_lds) and the input loads that follow it: the
+// counted `wait_vmcnt<N>` after those N loads retires the copy only if every one of them is issued AFTER
+// it (vmcnt retires in issue order).  LDS and global memory do not alias, so nothing else stops LLVM from
+// hoisting a buffer load above the copy: the empty asm with a memory clobber fences the IR passes, the
+// sched_barrier the machine scheduler.  tools/check_vmcnt.py audits the built ISA for it.
+__device__ __forceinline__ void dma_issue_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   const bf16x2_t v = __builtin_convertvector((float2_t){a, b}, bf16x2_t);
   return __builtin_bit_cast(unsigned, v);

@@ -116,7 +116,7 @@ def synth_batch(n_clips: int, n_samples: int, clip0: int, device) -> torch.Tenso
 
 
 def all_gather_codes(codes: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather one batch's (Nq, B, F) int64 codes over the process group -> (W, Nq, B, F).
+    """All-gather one batch's (Nq, B, F) int64 / int16 codes over the process group -> (W, Nq, B, F).
     Ranks must pass equal shapes (pad the last batch)."""
     import torch.distributed as dist
 
@@ -124,9 +124,11 @@ def all_gather_codes(codes: torch.Tensor, group=None) -> torch.Tensor:
         return codes.unsqueeze(0)
     world = dist.get_world_size(group)
     codes = codes.contiguous()
-    out = torch.empty((world * codes.shape[0],) + tuple(codes.shape[1:]), dtype=codes.dtype, device=codes.device)
-    dist.all_gather_into_tensor(out, codes, group=group)
-    return out.view((world,) + tuple(codes.shape))
+    # int16 (the on-disk type) travels as its bytes: RCCL and gloo have no 16-bit integer type
+    wire = codes.view(torch.int8) if codes.dtype == torch.int16 else codes
+    out = torch.empty((world * wire.shape[0],) + tuple(wire.shape[1:]), dtype=wire.dtype, device=wire.device)
+    dist.all_gather_into_tensor(out, wire, group=group)
+    return out.view(codes.dtype).view((world,) + tuple(codes.shape))
 
 
 def all_gather_status(status: torch.Tensor, group=None) -> torch.Tensor:
@@ -156,6 +158,87 @@ def _codes_of(out) -> torch.Tensor:
     return out["indices"] if isinstance(out, dict) else out
 
 
+def agreed_shape(stat: torch.Tensor):
+    """The (Nq, F) the batch's codes all-gather uses, decided from the gathered status table
+    stat (W, 4) = (ok, Nq, F, real clips) that EVERY rank holds, so every rank decides the same: the shape
+    of the most ok rows (ties: the lowest rank's).  Returns (nq, nf, ok mask of the rows that have it) or
+    None when no rank succeeded; an ok row with another shape is treated as a failed batch."""
+    ok = stat[:, 0].bool()
+    if not bool(ok.any()):
+        return None
+    shapes = [(int(stat[r, 1]), int(stat[r, 2])) for r in range(stat.shape[0]) if bool(ok[r])]
+    best = max(shapes, key=lambda sh: (shapes.count(sh), -shapes.index(sh)))
+    keep = ok & (stat[:, 1] == best[0]) & (stat[:, 2] == best[1])
+    return best[0], best[1], keep
+
+
+class _SinkWriter:
+    """Rank 0's host side of the extraction, off the critical path: the gathered codes are copied into a
+    pinned buffer on a side stream (ordered after the gather by an event), and a writer thread waits for
+    that copy, then hands every clip's (F, Nq) int16 array to the sink.  At most `depth` batches are queued;
+    errors in the sink are re-raised by flush()."""
+
+    def __init__(self, sink, depth: int = 4):
+        import queue
+        import threading
+
+        self.sink = sink
+        self.q = queue.Queue(maxsize=depth)
+        self.err = None
+        self.side = None
+        self.t = threading.Thread(target=self._loop, name="bigcodec-sink", daemon=True)
+        self.t.start()
+
+    def submit(self, gathered: torch.Tensor, rows):
+        """gathered (W, Nq, B, F) int16; rows = [(r, [(clip id, column j), ...]), ...] to sink."""
+        if self.err is not None:
+            raise self.err
+        if gathered.is_cuda:
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=gathered.device)
+            host = torch.empty(gathered.shape, dtype=gathered.dtype, pin_memory=True)
+            ev = torch.cuda.Event()
+            self.side.wait_stream(torch.cuda.current_stream(gathered.device))
+            with torch.cuda.stream(self.side):
+                host.copy_(gathered, non_blocking=True)
+                gathered.record_stream(self.side)
+                ev.record(self.side)
+        else:
+            host, ev = gathered.clone(), None
+        self.q.put((host, ev, rows))
+        return host
+
+    def _loop(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                self.q.task_done()
+                return
+            host, ev, rows = item
+            try:
+                if self.err is None:
+                    if ev is not None:
+                        ev.synchronize()
+                    arr = host.permute(0, 3, 2, 1).numpy()  # (W, F, B, Nq) view: arr[r, :, j] is clip j's (F, Nq)
+                    for r, clips in rows:
+                        for cid, j in clips:
+                            self.sink(cid, np.ascontiguousarray(arr[r, :, j]))
+            except BaseException as e:  # surfaced by submit / flush on the caller's thread
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def flush(self):
+        self.q.join()
+        if self.err is not None:
+            err, self.err = self.err, None
+            raise err
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+
+
 class ShardedExtractor:
     """Clip-sharded extraction of clips [0, n_clips) over `world` ranks.
 
@@ -164,16 +247,19 @@ class ShardedExtractor:
     the per-batch collectives line up.  A batch whose source or model raises is counted, not fatal
     (extract_indices.py:565-574) — and the failing rank STILL joins both of the batch's collectives:
     first an all-gather of (ok, Nq, F) per rank, then, if any rank succeeded, the all-gather of the
-    (Nq, B, F) codes, in which a failed rank contributes zeros of the agreed shape.  No rank can be
-    left waiting in a collective another rank skipped.
+    (Nq, B, F) codes as int16 (the on-disk type, extract_indices.py:532), in which a failed rank contributes
+    zeros of the agreed shape.  The agreed shape comes from the status table every rank holds
+    (agreed_shape), so a rank whose codes have another shape is counted as failed on every rank alike
+    and no rank can be left waiting in a collective another rank skipped.
 
     `source(clip0, n) -> (n, 1, T)` supplies a batch (default: bc_synth_clips on `device`);
     `model(x)` returns the codes (Nq, B, F) or a dict with "indices" (BigCodecModel);
     `sink(global_clip_id, codes (F, Nq) int16)` receives every successfully encoded clip of the job
-    on rank 0 (e.g. an .npy writer, save_indices)."""
+    on rank 0 (e.g. an .npy writer, save_indices), on a writer thread that runs behind the device (the
+    D2H copy and the sink overlap the next batches); run() / flush() wait for it."""
 
     def __init__(self, model, n_clips: int, n_samples: int, batch: int, rank: int = 0, world: int = 1,
-                 device=None, gather: bool = True, sink=None, group=None, source=None):
+                 device=None, gather: bool = True, sink=None, group=None, source=None, sink_depth: int = 4):
         if batch <= 0 or n_clips < 0:
             raise ValueError("batch must be > 0 and n_clips >= 0")
         self.model, self.n_clips, self.n_samples, self.batch = model, n_clips, n_samples, batch
@@ -184,11 +270,12 @@ class ShardedExtractor:
         per_rank = max(shard_range(n_clips, r, world)[1] - shard_range(n_clips, r, world)[0] for r in range(world))
         self.n_batches = (per_rank + batch - 1) // batch
         self.stats = ExtractStats()
-        self.last = None  # rank 0: the last batch's gathered (W, B, F, Nq) int16 host array
+        self.writer = _SinkWriter(sink, sink_depth) if (rank == 0 and sink is not None) else None
+        self.last = None  # rank 0: the last batch's gathered (W, Nq, B, F) int16 host tensor (filled behind the device)
 
     def step(self, bi: int):
-        """Batch `bi` of every rank: encode, gather, hand to the sink.  Returns the gathered
-        (W, Nq, B, F) device codes, or None when the batch failed on every rank."""
+        """Batch `bi` of every rank: encode, gather, queue for the sink.  Returns the gathered
+        (W, Nq, B, F) int16 device codes, or None when the batch failed on every rank."""
         st = self.stats
         s = self.lo + bi * self.batch
         real = max(0, min(s + self.batch, self.hi) - s)
@@ -199,46 +286,59 @@ class ShardedExtractor:
                 raise ValueError(f"model returned codes of shape {tuple(codes.shape)}, expected (Nq, {self.batch}, F)")
         except Exception:  # per-batch accounting, mirrors extract_indices.py:565-574
             codes = None
-            st.errors += real
-            st.error_items.extend(range(s, s + real))
         st.batches += 1
-        if codes is not None:
-            st.clips += real
-            st.frames += real * codes.shape[-1]
         gather = self.gather and self.world > 1
         dev = codes.device if codes is not None else self.device
         status = torch.tensor([1 if codes is not None else 0, codes.shape[0] if codes is not None else 0,
                                codes.shape[2] if codes is not None else 0, real], dtype=torch.int64)
         stat = all_gather_status(status.to(dev), self.group).cpu() if gather else status.unsqueeze(0)
-        ok = stat[:, 0].bool()
-        st.job_errors += int(stat[~ok, 3].sum())
-        st.job_clips += int(stat[ok, 3].sum())
-        if not bool(ok.any()):
+        agreed = agreed_shape(stat)
+        keep = agreed[2] if agreed is not None else torch.zeros(stat.shape[0], dtype=torch.bool)
+        me = self.rank if gather else 0
+        if bool(keep[me]):
+            st.clips += real
+            st.frames += real * codes.shape[-1]
+        else:  # failed here, or a shape the other ranks do not share: the batch's clips are lost
+            codes = None
+            st.errors += real
+            st.error_items.extend(range(s, s + real))
+        st.job_errors += int(stat[~keep, 3].sum())
+        st.job_clips += int(stat[keep, 3].sum())
+        if agreed is None:
             return None
-        first = int(torch.nonzero(ok)[0, 0])
-        nq, nf = int(stat[first, 1]), int(stat[first, 2])
-        if codes is None:
-            codes = torch.zeros((nq, self.batch, nf), dtype=torch.int64, device=dev)
-        elif (codes.shape[0], codes.shape[2]) != (nq, nf):
-            raise RuntimeError(f"rank {self.rank}: codes {tuple(codes.shape)} disagree with rank {first}'s "
-                               f"(Nq={nq}, F={nf}); every rank must encode the same clip length")
-        gathered = all_gather_codes(codes, self.group) if gather else codes.unsqueeze(0)
-        if self.rank == 0 and self.sink is not None:
-            arr = gathered.permute(0, 2, 3, 1).cpu().numpy().astype(np.int16)  # (W, B, F, Nq)
-            self.last = arr
-            for r in range(arr.shape[0]):
-                if not bool(ok[r]):
+        nq, nf = agreed[0], agreed[1]
+        codes16 = (torch.zeros((nq, self.batch, nf), dtype=torch.int16, device=dev) if codes is None
+                   else codes.to(torch.int16))  # extract_indices.py:532's astype(np.int16), on the device
+        gathered = all_gather_codes(codes16, self.group) if gather else codes16.unsqueeze(0)
+        if self.writer is not None:
+            rows = []
+            for r in range(gathered.shape[0]):
+                if not bool(keep[r if gather else 0]):
                     continue
                 rlo, rhi = shard_range(self.n_clips, r, self.world) if gather else (self.lo, self.hi)
                 rs = rlo + bi * self.batch
-                for j in range(self.batch):
-                    if rs + j < rhi:
-                        self.sink(rs + j, arr[r, j])
+                rows.append((r, [(rs + j, j) for j in range(self.batch) if rs + j < rhi]))
+            self.last = self.writer.submit(gathered, rows)
         return gathered
 
+    def flush(self):
+        """Wait until the sink has received every batch stepped so far (re-raises a sink error)."""
+        if self.writer is not None:
+            self.writer.flush()
+
+    def close(self):
+        if self.writer is not None:
+            self.writer.flush()
+            self.writer.close()
+            self.writer = None
+
     def run(self) -> ExtractStats:
-        for bi in range(self.n_batches):
-            self.step(bi)
+        try:
+            for bi in range(self.n_batches):
+                self.step(bi)
+            self.flush()
+        finally:
+            self.close()
         return self.stats
 
 

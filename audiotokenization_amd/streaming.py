@@ -66,6 +66,10 @@ class StreamingEncoder:
         return y
 
     def push(self, x) -> torch.Tensor:
+        with _lib.status_scope():
+            return self._push(x)
+
+    def _push(self, x) -> torch.Tensor:
         x = _as_input(x)
         if x.shape[-1] % self.hop:
             raise ValueError(f"chunk of {x.shape[-1]} samples: must be a multiple of the hop ({self.hop})")

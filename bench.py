@@ -431,6 +431,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(n_steps):
             codes = step()
+        if extractor is not None:
+            extractor.flush()  # rank 0's sink has received every timed batch (its writer thread runs behind)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

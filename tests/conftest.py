@@ -16,6 +16,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "reference: needs /root/reference (development container only)")
 
 
+# GPU modules run from the kernel level up (a kernel regression is reported by its own test before any
+# whole-model test trips over it), the full-size config runs last (they take the longest).  Stable: the
+# order within a module is unchanged; modules not listed keep their place before the listed ones.
+_GPU_ORDER = ["test_gpu_kernels", "test_gpu_ops", "test_gpu_fsq", "test_gpu_model", "test_gpu_tokens",
+              "test_gpu_streaming", "test_gpu_extract", "test_extract_cli", "test_gpu_full_size"]
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
 
@@ -23,6 +30,11 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords and not has_gpu:
             item.add_marker(pytest.mark.skip(reason="no HIP device"))
+
+    def key(item):
+        mod = item.module.__name__.rsplit(".", 1)[-1] if item.module else ""
+        return _GPU_ORDER.index(mod) + 1 if mod in _GPU_ORDER else 0
+    items.sort(key=key)
 
 
 def load_golden(name):

@@ -48,8 +48,29 @@ def max_rel_err(a, b) -> float:
     return float((a - b).abs().max() / scale)
 
 
-def assert_close_rel(a, b, tol: float, what: str = ""):
+def error_profile(a, b, top: int = 8) -> str:
+    """Where a (C, F) or (..., C, F) difference lives: the frames and channels with the largest |a - b|, the
+    error by frame decile and how many elements exceed 10x the median error -- so a failure in a race-free
+    kernel path (whole-tensor drift) reads differently from one bad lane / tile / time step."""
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    d = (a - b).abs().reshape(-1, a.shape[-2], a.shape[-1]).amax(0)  # (C, F)
+    by_f, by_c = d.amax(0), d.amax(1)
+    F = by_f.numel()
+    fi = torch.argsort(by_f, descending=True)[:top].tolist()
+    ci = torch.argsort(by_c, descending=True)[:top].tolist()
+    dec = [float(by_f[i * F // 10:(i + 1) * F // 10].max()) for i in range(10) if (i + 1) * F // 10 > i * F // 10]
+    med = float(d.median())
+    return ("worst frames " + ", ".join(f"{i}:{float(by_f[i]):.1e}(ch {int(d[:, i].argmax())})" for i in fi) +
+            "; worst channels " + ", ".join(f"{i}:{float(by_c[i]):.1e}" for i in ci) +
+            "; max by frame decile " + " ".join(f"{v:.1e}" for v in dec) +
+            f"; median {med:.1e}, {int((d > 10 * med).sum())} of {d.numel()} above 10x median")
+
+
+def assert_close_rel(a, b, tol: float, what: str = "", profile: bool = False):
     err = max_rel_err(a, b)
+    if err > tol and profile:
+        raise AssertionError(f"{what}: max |a-b| / max|b| = {err:.3e} > {tol:.1e}; {error_profile(a, b)}")
     assert err <= tol, f"{what}: max |a-b| / max|b| = {err:.3e} > {tol:.1e}"
 
 

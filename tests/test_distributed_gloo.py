@@ -168,3 +168,73 @@ def test_extract_sharded_single_process_no_dist():
     st = extract_sharded(lambda x: _fake_codes(x[:, 0, 0].long()), 7, 8, 3, device=torch.device("cpu"),
                          sink=lambda cid, arr: sunk.__setitem__(cid, arr), source=_fake_source)
     assert st.clips == 7 and st.errors == 0 and st.batches == 3 and sorted(sunk) == list(range(7))
+
+
+def _shape_worker(rank, world, port, q, odd_rank, odd_batch):
+    """A rank whose model returns codes of ANOTHER frame count for one batch (it used to raise
+    before the codes gather while the other ranks blocked in it)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from audiotokenization_amd.extract import extract_sharded
+
+    calls = {"n": 0}
+
+    def model(x):
+        bi = calls["n"]
+        calls["n"] += 1
+        c = _fake_codes(x[:, 0, 0].long())
+        if rank == odd_rank and bi == odd_batch:
+            c = torch.cat([c, c[..., :1]], dim=-1)  # F + 1 frames
+        return c
+
+    sunk = {}
+    st = extract_sharded(model, N_CLIPS, 8, BATCH, rank=rank, world=world, device=torch.device("cpu"),
+                         sink=lambda cid, arr: sunk.__setitem__(cid, arr.copy()), source=_fake_source)
+    q.put((rank, (st, sunk)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,odd_rank,odd_batch", [(2, 1, 0), (3, 1, 1), (3, 0, 0)])
+def test_extract_sharded_rank_with_other_frame_count(world, odd_rank, odd_batch):
+    """Every rank decides the codes gather's shape from the gathered status table (the shape most ranks
+    have; ties: the lowest rank's), so the job finishes; the odd rank's batch is counted as failed on
+    every rank and every other clip arrives with its own codes."""
+    from audiotokenization_amd.extract import shard_range
+
+    results = _run(_shape_worker, world, odd_rank, odd_batch)
+    olo, ohi = shard_range(N_CLIPS, odd_rank, world)
+    lost = list(range(olo + odd_batch * BATCH, min(olo + (odd_batch + 1) * BATCH, ohi)))
+    assert lost
+    for r in range(world):
+        st, sunk = results[r]
+        assert st.errors == (len(lost) if r == odd_rank else 0)
+        assert st.job_errors == len(lost) and st.job_clips == N_CLIPS - len(lost)
+        if r == 0:
+            assert sorted(sunk) == [c for c in range(N_CLIPS) if c not in lost]
+            for cid, arr in sunk.items():
+                np.testing.assert_array_equal(arr, _fake_codes([cid])[:, 0, :].T.numpy())
+
+
+def test_agreed_shape_rule():
+    from audiotokenization_amd.extract import agreed_shape
+
+    t = torch.tensor([[1, 1, 5, 3], [1, 1, 6, 3], [1, 1, 6, 2], [0, 0, 0, 3]])
+    nq, nf, keep = agreed_shape(t)
+    assert (nq, nf) == (1, 6) and keep.tolist() == [False, True, True, False]
+    nq, nf, keep = agreed_shape(torch.tensor([[1, 2, 7, 1], [1, 2, 8, 1]]))
+    assert (nq, nf) == (2, 7) and keep.tolist() == [True, False]
+    assert agreed_shape(torch.tensor([[0, 0, 0, 4], [0, 0, 0, 4]])) is None
+
+
+def test_sink_errors_surface():
+    """A sink that raises (e.g. a full disk) fails the extraction on the caller's thread."""
+    from audiotokenization_amd.extract import extract_sharded
+
+    def bad_sink(cid, arr):
+        raise OSError("disk full")
+
+    with pytest.raises(OSError, match="disk full"):
+        extract_sharded(lambda x: _fake_codes(x[:, 0, 0].long()), 7, 8, 3, device=torch.device("cpu"), sink=bad_sink,
+                        source=_fake_source)

@@ -131,19 +131,36 @@ def _full_model(dev, name="default"):
     return enc, dec, esd, dsd, ek, dk
 
 
-def test_full_size_batch_invariance_and_determinism(dev):
-    """BASELINE config 2 shape (10 s @24 kHz clips, default model): a clip's indices do not depend on
-    which batch it is encoded in, and repeated runs are bitwise identical."""
+@pytest.mark.parametrize("precision", ["h3", "x6"])
+def test_full_size_batch_invariance_and_determinism(dev, precision):
+    """BASELINE config 2 shape (10 s @24 kHz clips, default model): repeated runs give bitwise identical
+    LATENTS (every precision has a fixed accumulation order, so any difference is a race; a code-only check
+    misses a drift that moves no index), and a clip's indices do not depend on which batch it is
+    encoded in.  The first forward runs after a forward in the other precision, as in the suite's order."""
+    from audiotokenization_amd import _lib
     from audiotokenization_amd.extract import synth_batch
 
     enc, dec, *_ = _full_model(dev)
-    with torch.no_grad():
-        xb = synth_batch(8, 240000, 0, dev)
-        c1 = dec(enc(xb), vq=True)[1]
-        c2 = dec(enc(xb), vq=True)[1]
-        cs = torch.cat([dec(enc(xb[i:i + 1]), vq=True)[1] for i in (0, 5)], dim=1)
-        torch.cuda.synchronize()
+    old = _lib.precision_mode()
+    try:
+        with torch.no_grad():
+            xb = synth_batch(8, 240000, 0, dev)
+            _lib.set_precision("x6" if precision == "h3" else "h3")
+            enc(xb)  # leaves the other precision's data in every reused workspace
+            _lib.set_precision(precision)
+            l1 = enc(xb)
+            l2 = enc(xb)
+            c1 = dec(l1, vq=True)[1]
+            c2 = dec(l2, vq=True)[1]
+            cs = torch.cat([dec(enc(xb[i:i + 1]), vq=True)[1] for i in (0, 5)], dim=1)
+            torch.cuda.synchronize()
+    finally:
+        _lib._mode = old
     assert c1.shape == (1, 8, 1200)
+    if not torch.equal(l1, l2):
+        from helpers import error_profile
+
+        raise AssertionError(f"[{precision}] two forwards of one batch differ: {error_profile(l1, l2)}")
     assert torch.equal(c1, c2)
     assert torch.equal(c1[:, [0, 5]], cs)
     assert len(torch.unique(c1)) > 50
