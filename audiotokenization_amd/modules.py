@@ -148,6 +148,9 @@ class Snake(SnakeBeta):
         return self._cache.get(_pkey(self.alpha) + (str(device),), build)
 
 
+# Adopted, as the reference's vq/alias_free_torch/filter.py:25-27 states for its own copy, from adefossez's
+# julius.lowpass.LowPassFilters under the MIT License (https://adefossez.github.io/julius/julius/lowpass.html).
+# The buffer values must be bit-identical to the reference's (test_oracle_pinned.py), hence the same expression.
 def kaiser_sinc_filter1d(cutoff, half_width, kernel_size):
     """vq/alias_free_torch/filter.py:28-57 (init-time constant; returns (1,1,kernel_size))."""
     even = kernel_size % 2 == 0

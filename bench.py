@@ -112,7 +112,7 @@ def parse():
     p.add_argument("--cpu-clips", type=int, default=4, help="clips in the CPU-baseline B=1 sample (about 3 s each)")
     p.add_argument("--cpu-batches", default="4,16", help="batch sizes of the extra CPU-baseline calls ('' = none)")
     p.add_argument("--no-x6", action="store_true", help="skip the fp32-accurate x6 leg beside the h3 headline")
-    p.add_argument("--x6-steps", type=int, default=2)
+    p.add_argument("--x6-steps", type=int, default=None, help="timed steps of the x6 leg (default: --steps)")
     p.add_argument("--corpus", type=int, default=100_000, help="config 4: clips in the synthetic corpus")
     p.add_argument("--precision", choices=["fp32", "x6", "bf16", "h3"], default=None,
                    help="conv GEMM arithmetic (default: the config's, else BIGCODEC_PRECISION or h3)")
@@ -121,6 +121,7 @@ def parse():
     a.batch = a.batch or c["batch"]
     a.seconds = a.seconds or c["seconds"]
     a.precision = a.precision or c["precision"]
+    a.x6_steps = a.x6_steps or a.steps  # the x6 leg is timed over as many steps as the headline
     return a
 
 
@@ -544,10 +545,12 @@ def main():
                 parity["note"] = "waveforms compared end to end; equal codes make it the decoder's error alone"
     if rank == 0:
         prec = {"fp32": ("f32", "native fp32 MFMA (v_mfma_f32_16x16x4f32)"),
-                "x6": ("f32", "fp32-class: operands split exactly into 3 bf16 terms (24-bit), 6 bf16 MFMAs per "
-                              "product, fp32 accumulate"),
-                "h3": ("f32", "fp32-class: operands block-scaled and split into 2 fp16 terms (22-bit), 3 fp16 "
-                              "MFMAs per product (lo x lo dropped, < 2^-22 relative), fp32 accumulate"),
+                "x6": ("f32-emulated (x6: 3xbf16, 24-bit operands)",
+                       "fp32-class: operands split exactly into 3 bf16 terms (24-bit), 6 bf16 MFMAs per "
+                       "product, fp32 accumulate"),
+                "h3": ("f32-emulated (h3: 2xfp16, 22-bit operands)",
+                       "fp32-class: operands block-scaled and split into 2 fp16 terms (22-bit), 3 fp16 "
+                       "MFMAs per product (lo x lo dropped, < 2^-22 relative), fp32 accumulate"),
                 "bf16": ("bf16", "bf16 conv products (one bf16 MFMA per product), fp32 accumulate and storage; "
                                  "LSTM and VQ fp32-accurate")}[args.precision]
         line = {
