@@ -42,7 +42,7 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st);
 int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n);
 int conv_kernel_name(int cfg_id, int K, int s, int d, char* buf, int n);
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n);
-int resunit_rr_kernel_name(int C, char* buf, int n);
+int resunit_rr_kernel_name(int C, int d, char* buf, int n);
 long long conv_packed_floats(int Cout, int Cin, int K, int cfg_id);
 void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int cfg_id);
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);

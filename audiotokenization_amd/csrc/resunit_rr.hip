@@ -21,6 +21,7 @@
 // Weights use resunit_x6's packing for the unit's cfg (bc_conv1d_pack, one m-group of C rows).
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <type_traits>
 
 #include "bc_common.h"
@@ -173,8 +174,10 @@ __global__ void __launch_bounds__(64 * (C / 16) * WN, 2) resunit_rr_kernel(RRArg
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
           if (act_in) {  // out-of-range samples read 0 and snake(0) = 0: the reference's zero padding
-            v0[i][k] = snake(v0[i][k], a0, b0);
-            v1[i][k] = snake(v1[i][k], a1, b1);
+            // the two channels as one packed pair (bit-identical to snake() on each, half the VALU issue)
+            const f32x2 v = snake_pk((f32x2){v0[i][k], v1[i][k]}, (f32x2){a0, a1}, (f32x2){b0, b1});
+            v0[i][k] = v.x;
+            v1[i][k] = v.y;
           }
           const unsigned u0 = __float_as_uint(fabsf(v0[i][k])), u1 = __float_as_uint(fabsf(v1[i][k]));
           m = m > u0 ? m : u0;
@@ -298,17 +301,21 @@ __global__ void __launch_bounds__(64 * (C / 16) * WN, 2) resunit_rr_kernel(RRArg
     {
       const float xinv = 1.f / cur;
       unsigned m = 0;
+      // channels co4 + 2p, co4 + 2p + 1 as packed pairs (bit-identical to snake() per element)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int co = co4 + rr;
-        const float bias = r.b7 ? r.b7[co] : 0.f;
-        const float sc = r.w7sc[co] * xinv, sa = r.s2a[co], sb = r.s2b[co];
+      for (int pr = 0; pr < 2; ++pr) {
+        const int co = co4 + 2 * pr;
+        const f32x2 bias = r.b7 ? (f32x2){r.b7[co], r.b7[co + 1]} : (f32x2){0.f, 0.f};
+        const f32x2 sc = (f32x2){r.w7sc[co] * xinv, r.w7sc[co + 1] * xinv};
+        const f32x2 sa = {r.s2a[co], r.s2a[co + 1]}, sb = {r.s2b[co], r.s2b[co + 1]};
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          const float v = snake(acc[j][rr] * sc + bias, sa, sb);
-          acc[j][rr] = v;
-          const unsigned u = __float_as_uint(fabsf(v));
-          m = m > u ? m : u;
+          const f32x2 v = snake_pk((f32x2){acc[j][2 * pr], acc[j][2 * pr + 1]} * sc + bias, sa, sb);
+          acc[j][2 * pr] = v.x;
+          acc[j][2 * pr + 1] = v.y;
+          const unsigned u0 = __float_as_uint(fabsf(v.x)), u1 = __float_as_uint(fabsf(v.y));
+          m = m > u0 ? m : u0;
+          m = m > u1 ? m : u1;
         }
       }
       m = wave_max_u32(m);
@@ -372,6 +379,377 @@ __global__ void __launch_bounds__(64 * (C / 16) * WN, 2) resunit_rr_kernel(RRArg
 }
 
 // ------------------------------------------------------------------------------------------------
+// Streaming ("strip") ResidualUnit at C = 48 (round 3; VERDICT r02 item 4: resunit_rr at 0.145 of its
+// ceiling with 1.6x read amplification).  resunit_rr gives every 64-column tile its own workgroup, so each
+// one re-reads and re-activates a 6d-column halo (up to 84 % extra at d = 9), streams all k=7 weights from L2
+// into registers again (1 KB per output column, 2.7x the activation bytes) and runs stage -> k7 -> bridge ->
+// k1 -> epilogue as one dependent latency chain.  Here ONE workgroup per CU walks strips of consecutive
+// 128-column blocks of a clip:
+//   * the k=7 weights are copied into LDS once per workgroup (63 KB: the full chunk's 16x16x32 A fragments
+//     and the 16-channel tail's 16x16x16 ones, compacted), the k=1 weights live in registers;
+//   * every input sample is loaded and activated (snake on load) ONCE: block j + 1's new columns are loaded
+//     into registers while block j computes, and the 6d-column halo it shares with block j is kept in LDS
+//     in fp32 (activated) and re-split with block j + 1's own block scale;
+//   * the epilogue's residual is loaded before phase 2 and the next block's input before phase 1, so both
+//     latencies hide behind MFMAs.
+// Arithmetic per block is resunit_rr's: h3 planes with block scales (full chunk sf, tail min(sf, st)), the
+// tail on 16x16x16 MFMAs in its own accumulator combined exactly, bridge h = snake2(acc / scales + b7) with a
+// block scale over the h tile, k1 from the h tile, conv_epilogue (residual, bias, next Snake, dual).
+// ------------------------------------------------------------------------------------------------
+constexpr int RS_C = 48;
+constexpr int RS_BN = 128;                 // output columns per block
+constexpr int RS_NG = 4;                   // column groups of 32 columns (2 n-tiles) per block
+constexpr int RS_NT = 2;
+constexpr int RS_NW = 3 * RS_NG;           // 12 waves: m-tile q = w % 3, column group g = w / 3
+constexpr int RS_NTHR = 64 * RS_NW;        // 768 threads
+constexpr int RS_W7F = 7 * 2 * 3 * 1024;   // full-chunk k7 A fragments [tap][plane][m-tile][lane][16 B]
+constexpr int RS_W7T = 7 * 2 * 3 * 512;    // tail k7 A fragments [tap][plane][m-tile][lane][8 B]
+
+struct RSArgs {
+  const float* x;             // staged input: x_raw (snake on load: isa != nullptr) or x_act
+  const unsigned char* w7;    // packed k=7 planes of the unit's cfg ([chunk][tap][plane][m-tile][lane][8 fp16])
+  const unsigned char* w1;    // packed k=1 planes
+  const float* b7;
+  const float* w7sc;          // 1 / k=7 row scale
+  const float* s2a;
+  const float* s2b;
+  const float* isa;           // snake on load or nullptr
+  const float* isb;
+  long long xbs;
+  int T, pl, nblk, nstrip, nwork;  // blocks per strip, strips per clip, B * nstrip
+};
+
+__host__ __device__ constexpr size_t rs_lds_bytes(int D) {
+  return (size_t)RS_W7F + RS_W7T + 2 * (size_t)(RS_BN + 6 * D) * 96 + 2 * (size_t)RS_C * 6 * D * 4;
+}
+
+template <int D>
+__global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, ConvArgs e) {
+  constexpr int C = RS_C, NT = RS_NT;
+  constexpr int HC = 6 * D;                 // halo columns shared by consecutive blocks
+  constexpr int W = RS_BN + HC;             // input window columns of a block
+  constexpr int BPL = W * 96;               // bytes per input plane: full chunk [W][64 B], tail [W][32 B]
+  constexpr int TB = W * 64;
+  constexpr int HPL = RS_BN * 96, HTB = RS_BN * 64;  // h tile (aliases the input planes)
+  constexpr int KH = (C * HC + RS_NTHR - 1) / RS_NTHR;       // halo samples per thread at a strip start
+  constexpr int KI = (24 * HC + RS_NTHR - 1) / RS_NTHR;      // halo channel pairs per thread to split
+  static_assert(RS_BN >= HC, "the next halo lies inside a block's new columns");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_rs[];
+  unsigned char* W7 = smem_rs;
+  unsigned char* PL = smem_rs + RS_W7F + RS_W7T;
+  float* HL = reinterpret_cast<float*>(PL + 2 * BPL);  // 2 x [C][HC] activated fp32 halo
+  __shared__ unsigned smx[2][RS_NW];
+  __shared__ unsigned hmx[RS_NW];
+  __shared__ float sisa[C], sisb[C];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = wave % 3, g = wave / 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const bool act_in = r.isa != nullptr;
+  const int G = gridDim.x;
+  int wi = xcd_remap(blockIdx.x, G);
+  if (wi >= r.nwork) return;  // uniform per workgroup
+
+  // ---- once per workgroup: Snake-on-load coefficients, k=7 weights -> LDS, k=1 weights -> registers ----
+  for (int c = tid; c < C; c += RS_NTHR) {
+    sisa[c] = act_in ? r.isa[c] : 0.f;
+    sisb[c] = act_in ? r.isb[c] : 0.f;
+  }
+  for (int u = tid; u < RS_W7F / 16; u += RS_NTHR)  // chunk 0 of the packing is already [tap][plane][m-tile][lane]
+    *reinterpret_cast<f16x8_t*>(W7 + u * 16) = *reinterpret_cast<const f16x8_t*>(r.w7 + u * 16);
+  for (int u = tid; u < RS_W7F / 16; u += RS_NTHR) {  // tail: the 16x16x16 operand gathered out of padded chunk 1
+    const int L = u & 63, tpq = u >> 6;               // tpq = (tap * 2 + plane) * 3 + m-tile
+    const int qq = tpq % 3, tp2 = tpq / 3;
+    const unsigned char* src = r.w7 + (long long)(7 + (tp2 >> 1)) * (2 * 3 * 1024) + (tp2 & 1) * 3 * 1024 + qq * 1024 +
+                               ((L & 15) + 16 * ((L >> 4) >> 1)) * 16 + 8 * ((L >> 4) & 1);
+    *reinterpret_cast<f16x4_t*>(W7 + RS_W7F + u * 8) = *reinterpret_cast<const f16x4_t*>(src);
+  }
+  f16x8_t U[2];
+  f16x4_t UT[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    U[p] = *reinterpret_cast<const f16x8_t*>(r.w1 + ((0 * 2 + p) * 3 + q) * 1024 + lane * 16);
+    UT[p] = *reinterpret_cast<const f16x4_t*>(r.w1 + ((1 * 2 + p) * 3 + q) * 1024 + (lr + 16 * (lg >> 1)) * 16 + 8 * (lg & 1));
+  }
+
+  // ---- block geometry: work item wi = (clip, strip), blocks of RS_BN output columns ----
+  const int nbt = (r.T + RS_BN - 1) / RS_BN;  // blocks per clip
+  auto strip_blocks = [&](int w) {
+    const int si = w % r.nstrip;
+    const int n = nbt - si * r.nblk;
+    return n < r.nblk ? n : r.nblk;
+  };
+  auto block_col = [&](int w, int blk) { return ((w % r.nstrip) * r.nblk + blk) * RS_BN; };  // first output column
+
+  // staging threads: channel pair sp (24), column lane cl: new columns HC + cl + 32 i of the window
+  const int sp = tid >> 5, cl = tid & 31;
+  float n0[4], n1[4], hv[KH];
+  auto prefetch = [&](int w, int blk) {
+    const int b = w / r.nstrip;
+    const int ws = block_col(w, blk) - r.pl;  // clip column of window column 0
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(r.x + (long long)b * r.xbs), 0, C * r.T * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = ws + HC + cl + 32 * i;
+      const bool ok = t >= 0 && t < r.T;
+      const unsigned o = ok ? (unsigned)((2 * sp * r.T + t) * 4) : 0xfffffff0u;
+      n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
+      n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? o + (unsigned)r.T * 4 : o, 0, 0));
+    }
+    if (blk == 0) {  // a strip's first block also needs the halo (window columns [0, HC))
+#pragma unroll
+      for (int k = 0; k < KH; ++k) {
+        const int el = tid + RS_NTHR * k;
+        const int ch = el / HC, t = ws + el % HC;
+        const bool ok = el < C * HC && t >= 0 && t < r.T;
+        hv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? (unsigned)((ch * r.T + t) * 4) : 0xfffffff0u, 0, 0));
+      }
+    }
+  };
+
+  int blk = 0, par = 0;
+  prefetch(wi, 0);
+  lds_barrier();  // coefficients and weights in LDS
+  while (true) {
+    const int b = wi / r.nstrip;
+    const int oj = block_col(wi, blk);
+    const int nbs = strip_blocks(wi);
+    float* hcur = HL + par * C * HC;
+    float* hnext = HL + (par ^ 1) * C * HC;
+
+    // ---------------- stage: activate the new columns, block maxima, split the window into LDS ----------------
+    if (blk == 0) {
+#pragma unroll
+      for (int k = 0; k < KH; ++k) {
+        const int el = tid + RS_NTHR * k;
+        if (el < C * HC) {
+          const int ch = el / HC;
+          hcur[el] = act_in ? snake(hv[k], sisa[ch], sisb[ch]) : hv[k];
+        }
+      }
+      lds_barrier();
+    }
+    const bool tailp = sp >= 16;  // channels 32..47: the tail chunk
+    {
+      const f32x2 ca = {sisa[2 * sp], sisa[2 * sp + 1]}, cb = {sisb[2 * sp], sisb[2 * sp + 1]};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (act_in) {  // zero samples (outside the clip) stay zero: snake(0) = 0, the reference's padding
+          const f32x2 v = snake_pk((f32x2){n0[i], n1[i]}, ca, cb);
+          n0[i] = v.x;
+          n1[i] = v.y;
+        }
+      }
+    }
+    unsigned mf = 0, mt = 0;
+    auto upd = [&](bool tl, float v) {
+      const unsigned u = __float_as_uint(fabsf(v));
+      if (tl) mt = mt > u ? mt : u;
+      else mf = mf > u ? mf : u;
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      upd(tailp, n0[i]);
+      upd(tailp, n1[i]);
+    }
+    float h0v[KI], h1v[KI];
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int el = tid + RS_NTHR * k;
+      h0v[k] = h1v[k] = 0.f;
+      if (el < 24 * HC) {
+        const int pe = el / HC, ce = el % HC;
+        h0v[k] = hcur[(2 * pe) * HC + ce];
+        h1v[k] = hcur[(2 * pe + 1) * HC + ce];
+        upd(pe >= 16, h0v[k]);
+        upd(pe >= 16, h1v[k]);
+      }
+    }
+    mf = wave_max_u32(mf);
+    mt = wave_max_u32(mt);
+    if (lane == 0) {
+      smx[0][wave] = mf;
+      smx[1][wave] = mt;
+    }
+    lds_barrier();  // also: every wave has finished the previous block's phase 2 (the h tile is dead)
+    float sf, st;
+    {
+      unsigned a = smx[0][0], c2 = smx[1][0];
+#pragma unroll
+      for (int w = 1; w < RS_NW; ++w) {
+        a = a > smx[0][w] ? a : smx[0][w];
+        c2 = c2 > smx[1][w] ? c2 : smx[1][w];
+      }
+      sf = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(a));
+      const float s2 = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(c2));
+      st = s2 < sf ? s2 : sf;  // resunit_rr's running minimum over the chunks
+    }
+    auto put = [&](int pr, int col, float v0, float v1) {  // channel pair pr at window column col
+      unsigned h, l;
+      if (pr < 16) {
+        split2_h(v0 * sf, v1 * sf, h, l);
+        unsigned char* dst = PL + rr_bfull(col, pr >> 2) + (pr & 3) * 4;
+        *reinterpret_cast<unsigned*>(dst) = h;
+        *reinterpret_cast<unsigned*>(dst + BPL) = l;
+      } else {
+        split2_h(v0 * st, v1 * st, h, l);
+        unsigned char* dst = PL + TB + rr_btail(col, (pr - 16) >> 2) + ((pr - 16) & 3) * 4;
+        *reinterpret_cast<unsigned*>(dst) = h;
+        *reinterpret_cast<unsigned*>(dst + BPL) = l;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = HC + cl + 32 * i;
+      put(sp, col, n0[i], n1[i]);
+      if (col >= RS_BN) {  // the next block's halo: this window's columns [RS_BN, W)
+        hnext[(2 * sp) * HC + col - RS_BN] = n0[i];
+        hnext[(2 * sp + 1) * HC + col - RS_BN] = n1[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int el = tid + RS_NTHR * k;
+      if (el < 24 * HC) put(el / HC, el % HC, h0v[k], h1v[k]);
+    }
+    lds_barrier();  // the window's planes are complete
+
+    // ---------------- the next block's input: in flight while this block computes ----------------
+    int nwi = wi, nblk_ = blk + 1;
+    if (nblk_ >= nbs) {
+      nwi = wi + G;
+      nblk_ = 0;
+    }
+    if (nwi < r.nwork) prefetch(nwi, nblk_);
+    // the epilogue's residual (16-byte groups of the lanes / tiles that take the vector path)
+    floatx4 rpre[NT];
+    {
+      const float* rb = e.res ? e.res + (long long)b * e.rbs : nullptr;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int co = q * 16 + lr;
+        const int nb = oj + g * 32 + j * 16 + lg * 4;
+        rpre[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (rb && e.vec && nb + 3 < e.Nout) rpre[j] = *reinterpret_cast<const floatx4*>(rb + (long long)co * e.yT + e.ooff + nb);
+      }
+    }
+
+    // ---------------- phase 1: k=7, m-tile q x columns [32 g, 32 g + 32) ----------------
+    floatx4 acc[NT], acct[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = acct[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int col0 = g * 32 + lr;
+#pragma unroll 1
+    for (int t = 0; t < 7; ++t) {
+      const f16x8_t a0 = *reinterpret_cast<const f16x8_t*>(W7 + ((t * 2 + 0) * 3 + q) * 1024 + lane * 16);
+      const f16x8_t a1 = *reinterpret_cast<const f16x8_t*>(W7 + ((t * 2 + 1) * 3 + q) * 1024 + lane * 16);
+      rr_taps(acc, PL, BPL, col0 + t * D, lg, a0, a1);
+      const f16x4_t at0 = *reinterpret_cast<const f16x4_t*>(W7 + RS_W7F + ((t * 2 + 0) * 3 + q) * 512 + lane * 8);
+      const f16x4_t at1 = *reinterpret_cast<const f16x4_t*>(W7 + RS_W7F + ((t * 2 + 1) * 3 + q) * 512 + lane * 8);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int off = rr_btail(col0 + 16 * j + t * D, lg >> 1) + 8 * (lg & 1);
+        const f16x4_t b0 = *reinterpret_cast<const f16x4_t*>(PL + TB + off);
+        const f16x4_t b1 = *reinterpret_cast<const f16x4_t*>(PL + BPL + TB + off);
+        floatx4 v = acct[j];
+        v = __builtin_amdgcn_mfma_f32_16x16x16f16(at1, b0, v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x16f16(at0, b1, v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x16f16(at0, b0, v, 0, 0, 0);
+        acct[j] = v;
+      }
+    }
+    {  // powers of two: exact
+      const float rs = st < sf ? st / sf : 1.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = acc[j] * rs + acct[j];
+    }
+
+    // ---------------- bridge: h = snake2(acc / (st * w7 scale) + b7), tile scale, split ----------------
+    const int co4 = q * 16 + 4 * lg;
+    {
+      const float xinv = 1.f / st;
+      unsigned m = 0;
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int co = co4 + 2 * pr;
+        const f32x2 bias = r.b7 ? (f32x2){r.b7[co], r.b7[co + 1]} : (f32x2){0.f, 0.f};
+        const f32x2 sc = (f32x2){r.w7sc[co] * xinv, r.w7sc[co + 1] * xinv};
+        const f32x2 sa = {r.s2a[co], r.s2a[co + 1]}, sb = {r.s2b[co], r.s2b[co + 1]};
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const f32x2 v = snake_pk((f32x2){acc[j][2 * pr], acc[j][2 * pr + 1]} * sc + bias, sa, sb);
+          acc[j][2 * pr] = v.x;
+          acc[j][2 * pr + 1] = v.y;
+          const unsigned u0 = __float_as_uint(fabsf(v.x)), u1 = __float_as_uint(fabsf(v.y));
+          m = m > u0 ? m : u0;
+          m = m > u1 ? m : u1;
+        }
+      }
+      m = wave_max_u32(m);
+      if (lane == 0) hmx[wave] = m;
+    }
+    lds_barrier();  // every wave is past phase 1: the input planes are dead, the h tile may overwrite them
+    float hs;
+    {
+      unsigned mm = hmx[0];
+#pragma unroll
+      for (int w = 1; w < RS_NW; ++w) mm = mm > hmx[w] ? mm : hmx[w];
+      hs = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(mm));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = col0 + 16 * j;
+      unsigned h0, l0, h1, l1;
+      split2_h(acc[j][0] * hs, acc[j][1] * hs, h0, l0);
+      split2_h(acc[j][2] * hs, acc[j][3] * hs, h1, l1);
+      unsigned char* dst;
+      if (co4 < 32) {
+        dst = PL + rr_hfull(n, co4 / 8) + (co4 % 8) * 2;
+      } else {
+        const int ct = co4 - 32;
+        dst = PL + HTB + rr_btail(n, ct / 8) + (ct % 8) * 2;
+      }
+      *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){h0, h1};
+      *reinterpret_cast<u32x2_t*>(dst + HPL) = (u32x2_t){l0, l1};
+    }
+    lds_barrier();
+
+    // ---------------- phase 2: k=1 from the h tile (input as the MFMA A operand: transposed output) ----------------
+    floatx4 acc2[1][NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = col0 + 16 * j;
+      const unsigned char* src = PL + rr_hfull(n, lg);
+      const f16x8_t h0 = *reinterpret_cast<const f16x8_t*>(src);
+      const f16x8_t h1 = *reinterpret_cast<const f16x8_t*>(src + HPL);
+      floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+      v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0, U[1], v, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h1, U[0], v, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0, U[0], v, 0, 0, 0);
+      const unsigned char* srt = PL + HTB + rr_btail(n, lg >> 1) + 8 * (lg & 1);
+      const f16x4_t t0 = *reinterpret_cast<const f16x4_t*>(srt);
+      const f16x4_t t1 = *reinterpret_cast<const f16x4_t*>(srt + HPL);
+      floatx4 vt = floatx4{0.f, 0.f, 0.f, 0.f};  // own accumulator (see resunit_rr phase 1)
+      vt = __builtin_amdgcn_mfma_f32_16x16x16f16(t0, UT[1], vt, 0, 0, 0);
+      vt = __builtin_amdgcn_mfma_f32_16x16x16f16(t1, UT[0], vt, 0, 0, 0);
+      vt = __builtin_amdgcn_mfma_f32_16x16x16f16(t0, UT[0], vt, 0, 0, 0);
+      acc2[0][j] = v + vt;
+    }
+    conv_epilogue_res<NT, true>(e, acc2, b, q * 16, oj + g * 32, lane, 1.f / hs, rpre);
+
+    // ---------------- next block ----------------
+    par ^= 1;
+    if (++blk >= nbs) {
+      wi += G;
+      blk = 0;
+      if (wi >= r.nwork) break;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
 // BC_RU_RR=0 keeps every unit on resunit_x6 (A/B timing).
@@ -384,6 +762,54 @@ static bool rr_enabled() {
 }
 
 bool resunit_rr_ok(int C, int d) { return rr_enabled() && C == 48 && d >= 1 && d <= RR_MAX_DIL; }
+
+// BC_RU_STRIP=0 keeps the C = 48 units on resunit_rr (A/B timing); BC_RU_STRIP_NBLK = blocks per strip.
+static bool strip_enabled() {
+  static const bool v = [] {
+    const char* s = getenv("BC_RU_STRIP");
+    return !s || atoi(s) != 0;
+  }();
+  return v;
+}
+static int strip_nblk() {
+  static const int v = [] {
+    const char* s = getenv("BC_RU_STRIP_NBLK");
+    const int n = s ? atoi(s) : 0;
+    return n > 0 ? n : 8;
+  }();
+  return v;
+}
+static bool strip_ok(int C, int d) { return strip_enabled() && C == RS_C && (d == 1 || d == 3 || d == 9); }
+
+static int strip_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return v;
+  }();
+  return n;
+}
+
+template <int D>
+static int launch_strip(RSArgs& r, ConvArgs& e, int B, hipStream_t st) {
+  const int nbt = (r.T + RS_BN - 1) / RS_BN;
+  r.nblk = strip_nblk();
+  r.nstrip = (nbt + r.nblk - 1) / r.nblk;
+  const long long nwork = (long long)B * r.nstrip;
+  if (nwork <= 0) return BC_OK;
+  if (nwork > 0x7fffffffLL || (long long)RS_C * r.T * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  r.nwork = (int)nwork;
+  const size_t lds = rs_lds_bytes(D);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resunit_strip_kernel<D>, RS_NTHR, lds) != hipSuccess ||
+      per_cu < 1)
+    return BC_ERR_UNSUPPORTED;
+  const long long grid = std::min<long long>(nwork, (long long)per_cu * std::max(1, strip_cus()));
+  hipLaunchKernelGGL(resunit_strip_kernel<D>, dim3((unsigned)grid), dim3(RS_NTHR), lds, st, r, e);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
 
 template <int C, int NT, int WN>
 static int launch_rr(RRArgs& r, ConvArgs& e, int B, hipStream_t st) {
@@ -405,9 +831,10 @@ static int launch_rr(RRArgs& r, ConvArgs& e, int B, hipStream_t st) {
   return BC_OK;
 }
 
-int resunit_rr_kernel_name(int C, char* buf, int n) {
+int resunit_rr_kernel_name(int C, int d, char* buf, int n) {
   if (C != 48) return -1;
-  return snprintf(buf, n, "resunit_rr_kernel<48, 4, 1>");  // the launch below
+  if (strip_ok(C, d)) return snprintf(buf, n, "resunit_strip_kernel<%d>", d);  // the launches below
+  return snprintf(buf, n, "resunit_rr_kernel<48, 4, 1>");
 }
 
 // x_raw / x_act / isa as resunit_launch; w7 / w1 packed for a resunit cfg whose tile has BM = C (one m-group)
@@ -437,6 +864,14 @@ int resunit_rr_launch(const float* x_raw, const float* x_act, const float* w7, c
   e.Cout = C; e.Nout = T; e.yT = T; e.ostride = 1; e.ooff = 0; e.epi = 0;
   e.wsc = reinterpret_cast<const float*>(r.w1 + (long long)nck * 2 * QA * 1024);
   e.vec = conv_epilogue_vec_ok(e);
+  if (strip_ok(C, d)) {
+    RSArgs s{};
+    s.x = r.x; s.w7 = r.w7; s.w1 = r.w1; s.b7 = b7; s.w7sc = r.w7sc; s.s2a = s2a; s.s2b = s2b;
+    s.isa = isa; s.isb = isb; s.xbs = r.xbs; s.T = T; s.pl = pl;
+    if (d == 1) return launch_strip<1>(s, e, B, st);
+    if (d == 3) return launch_strip<3>(s, e, B, st);
+    return launch_strip<9>(s, e, B, st);
+  }
   // measured (tools/ru_rr_sweep.sh, profiles/r02_ru_rr_sweep.txt): 4 n-tiles per wave, one column group
   // (BN = 64, 3 waves): 5.25-5.36 ms vs 5.45-5.74 for resunit_x6 at C = 48, T = 240 000, B = 64; every
   // variant lost at C = 96 (7.1-11 ms vs 6.5), which stays on resunit_x6

@@ -146,9 +146,10 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
     const float a0 = ci0 < a.Cin ? r.isa[ci0] : 0.f, b0 = ci0 < a.Cin ? r.isb[ci0] : 0.f;
     const float a1 = ci0 + 1 < a.Cin ? r.isa[ci0 + 1] : 0.f, b1 = ci0 + 1 < a.Cin ? r.isb[ci0 + 1] : 0.f;
 #pragma unroll
-    for (int i = 0; i < CI; ++i) {
-      bv0[i] = snake(bv0[i], a0, b0);
-      bv1[i] = snake(bv1[i], a1, b1);
+    for (int i = 0; i < CI; ++i) {  // the two channels as one packed pair (bit-identical to snake() on each)
+      const f32x2 v = snake_pk((f32x2){bv0[i], bv1[i]}, (f32x2){a0, a1}, (f32x2){b0, b1});
+      bv0[i] = v.x;
+      bv1[i] = v.y;
     }
   };
   auto store_b = [&]() {
@@ -313,15 +314,19 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       const int co = wm * MT * 16 + i * 16 + (lane >> 4) * 4;
       if (co >= C) continue;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float bias = a.bias ? a.bias[co + q] : 0.f;
-        const float sc = a.wsc[co + q] * xinv, sa = r.s2a[co + q], sb = r.s2b[co + q];
+      for (int pr = 0; pr < 2; ++pr) {  // channels co + 2 pr, co + 2 pr + 1 as packed pairs (bit-identical)
+        const int c0 = co + 2 * pr;
+        const f32x2 bias = a.bias ? (f32x2){a.bias[c0], a.bias[c0 + 1]} : (f32x2){0.f, 0.f};
+        const f32x2 sc = {a.wsc[c0] * xinv, a.wsc[c0 + 1] * xinv};
+        const f32x2 sa = {r.s2a[c0], r.s2a[c0 + 1]}, sb = {r.s2b[c0], r.s2b[c0 + 1]};
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          const float v = snake(acc[i][j][q] * sc + bias, sa, sb);
-          acc[i][j][q] = v;
-          const unsigned u = __float_as_uint(fabsf(v));
-          m = m > u ? m : u;
+          const f32x2 v = snake_pk((f32x2){acc[i][j][2 * pr], acc[i][j][2 * pr + 1]} * sc + bias, sa, sb);
+          acc[i][j][2 * pr] = v.x;
+          acc[i][j][2 * pr + 1] = v.y;
+          const unsigned u0 = __float_as_uint(fabsf(v.x)), u1 = __float_as_uint(fabsf(v.y));
+          m = m > u0 ? m : u0;
+          m = m > u1 ? m : u1;
         }
       }
     }
@@ -523,7 +528,7 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const bool h3 = cfg >= 300 && cfg < 400;
   if (!(h3 || (cfg >= 100 && cfg < 200)) || cfg != resunit_select_cfg(C, d, h3 ? 3 : 1)) return -1;
-  if (h3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, buf, n);
+  if (h3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
   return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, h3 ? 2 : 3,
                   ru_tps(t, C, d, h3 ? 2 : 3));

@@ -354,6 +354,47 @@ def test_resunit_fused(dev, C, d, causal, B, T, ru_prec):
     assert torch.equal(lraw.cpu(), got) and torch.equal(lact.cpu(), act.cpu())
 
 
+@pytest.mark.parametrize("d,B,T", [(3, 1, 1001), (3, 1, 4096), (1, 1, 24000), (9, 1, 24000), (3, 2, 700),
+                                   (2, 1, 1001), (4, 1, 1001), (5, 1, 1001), (9, 2, 129), (1, 3, 128), (3, 1, 5)])
+def test_resunit_c48_h3_sweep(dev, d, B, T):
+    """The C = 48 units in h3 (the streaming strip kernel at d = 1 / 3 / 9, resunit_rr at other dilations) over
+    dilations, clip lengths around the 128-column block and strip boundaries, and batch sizes: against the
+    oracle, and snake on load bit-identical to a producer-side Snake (tools/ru_rr_check.py's sweep).
+    A failure prints the bad columns / channels."""
+    old = L.precision_mode()
+    L.set_precision("h3")
+    try:
+        g = torch.Generator().manual_seed(480 + d * 7 + T)
+        ru = BL.ResidualUnit(48, dilation=d)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            s_ = _snake(48, g)
+            ru.block[k].act.load_state_dict(s_.state_dict())
+        nxt = M.Activation1d(activation=_snake(48, g))
+        x = torch.randn(B, 48, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        want = O.residual_unit(x, sd, "", d, False, False)
+        want_s = O.snake_beta(want, nxt.act.alpha.detach(), nxt.act.beta.detach())
+        ru.to(dev)
+        nxt.to(dev)
+        xd = x.to(dev)
+        lazy = ru.flow(xd, None)[0].cpu()
+        eager = ru.flow(xd, ru.first_act(xd))[0].cpu()
+        lraw, lact = ru.flow(xd, None, want_raw=True, next_act=nxt)
+        name = L.resunit_kernel_name(ru._fused_cfg(), 48, d)
+    finally:
+        L._mode = old
+    bad = (lazy - want).abs() > 1e-4 * want.abs().max()
+    cols = torch.nonzero(bad.any(1).any(0)).flatten()
+    chans = torch.nonzero(bad.any(2).any(0)).flatten()
+    print(f"C=48 d={d} B={B} T={T} ({name}): bad cols {cols[:10].tolist()} (n={cols.numel()}), chans {chans[:12].tolist()}")
+    assert_close_rel(lazy, want, 2e-5, f"resunit C=48 d={d} T={T}")
+    assert torch.equal(lazy, eager)
+    assert torch.equal(lraw.cpu(), lazy)
+    assert_close_rel(lact.cpu(), want_s, 5e-5, "resunit C=48 + next snake")
+
+
 @pytest.mark.parametrize("Cin,Cout,K,s,d", [(384, 384, 7, 1, 9), (48, 96, 4, 2, 1), (768, 768, 1, 1, 1)])
 def test_bf16_precision_error(dev, Cin, Cout, K, s, d):
     """precision 'bf16' (config 5): one bf16 product per pair, fp32 accumulation.  Its error against

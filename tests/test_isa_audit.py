@@ -1,6 +1,11 @@
-"""ISA audit of the built HIP objects: every hand-counted `s_waitcnt vmcnt(N)` that follows
-an LDS-DMA weight copy must find that copy retired, i.e. the compiler must have issued every input load the count
-assumes AFTER the copy (tools/check_vmcnt.py: CFG walk over the disassembled gfx950 code objects)."""
+"""ISA audits of the built HIP objects (tools/check_vmcnt.py, tools/isa_repro/check_mfma_mix.py):
+
+  * every hand-counted `s_waitcnt vmcnt(N)` that follows an LDS-DMA weight copy must find that copy retired, i.e.
+    the compiler must have issued every input load the count assumes AFTER the copy;
+  * no MFMA may read as SrcC the vDST of a recent MFMA of ANOTHER opcode: hipcc (ROCm 7.2) puts no wait state
+    between them (it treats an exact SrcC overlap as forwarded), and on the MI355X that chain needs 4-5 wait states
+    (tools/isa_repro/run_chain_probe.py: 16x16x16 -> 16x16x32 wrong on ~99 % of waves below 5 states, 16x16x32 ->
+    16x16x16 on a few waves in 16 384 below 4) -- the cause of resunit_rr's "intermittently wrong lanes" (ADVICE r02)."""
 import concurrent.futures as cf
 import os
 import sys
@@ -10,7 +15,10 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(REPO, "audiotokenization_amd", "_build")
 OBJECTS = ["conv1d_x6_p1.o", "conv1d_x6_p2.o", "conv1d_x6_p3.o", "resunit_x6.o"]
+MFMA_OBJECTS = ["conv1d.o", "conv1d_x6_p1.o", "conv1d_x6_p2.o", "conv1d_x6_p3.o", "resunit_x6.o", "resunit_rr.o",
+                "lstm.o", "lstm_seq.o", "vq.o", "elementwise.o", "resample.o", "probe.o"]
 sys.path.insert(0, os.path.join(REPO, "tools"))
+sys.path.insert(0, os.path.join(REPO, "tools", "isa_repro"))
 
 
 def _audit(obj):
@@ -43,3 +51,22 @@ def test_counted_vmcnt_waits_retire_the_lds_dma_copies():
         assert not hazards, "\n".join(hazards[:10])
         total += waits
     assert total > 500
+
+
+def _mix(obj):
+    import check_mfma_mix as cm
+    import check_vmcnt as cv
+
+    return obj, cm.scan(cv.disassemble(os.path.join(BUILD, obj)))
+
+
+def test_no_mixed_opcode_mfma_accumulator_chains():
+    import check_vmcnt as cv
+
+    missing = [o for o in MFMA_OBJECTS if not os.path.exists(os.path.join(BUILD, o))]
+    if missing or not os.path.exists(os.path.join(cv.LLVM, "llvm-objdump")):
+        pytest.skip(f"built objects / ROCm llvm tools not present ({missing})")
+    with cf.ProcessPoolExecutor(max_workers=4) as ex:
+        results = list(ex.map(_mix, MFMA_OBJECTS))
+    bad = [b for _, found in results for b in found]
+    assert not bad, "\n".join(bad[:10])
