@@ -31,24 +31,30 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 namespace bc {
 
 // sin(x) for the Snake: Cody-Waite reduction by pi in 4 fma steps (valid for |x| < 39000), odd
-// degree-9 minimax polynomial on [-pi/2, pi/2] — the published SLEEF xsinf (u3.5) algorithm and
-// constants — about 20 instructions instead of OCML sinf's ~150 with its Payne-Hanek path.  Inputs
+// degree-9 minimax polynomial on [-pi/2, pi/2] -- the published SLEEF xsinf (u3.5) algorithm and
+// constants -- about 20 instructions instead of OCML sinf's ~150 with its Payne-Hanek path.  Inputs
 // outside the reduction range (never produced by the codec's activations) take sinf.
-// Accuracy <= 3.5 ulp (tests/test_gpu_kernels.py::test_fast_sin measures it against fp64).
+// Accuracy <= 3.5 ulp (tests/test_gpu_kernels.py::test_snake measures it against fp64).
+// Round 3: q = rint(x / pi) as (t + 1.5 * 2^23) - 1.5 * 2^23 (round-to-nearest-even, exact for |t| < 2^22, so
+// equal to rintf), whose low mantissa bit is q's parity; the odd-q sign is applied to the RESULT by an xor
+// instead of negating d first: fma(s, u * (-d), -d) = -fma(s, u * d, d) exactly (s = d * d), so the value is
+// bit-identical to the previous rintf / cvt / and / cmp / negate / select form, in 5 fewer instructions.
+constexpr float BC_RINT_MAGIC = 12582912.0f;  // 1.5 * 2^23
 __device__ __forceinline__ float bc_sin(float x) {
   if (!(fabsf(x) < 39000.0f)) return sinf(x);
-  const float q = rintf(x * 0.318309886183790671538f);
+  const float qm = x * 0.318309886183790671538f + BC_RINT_MAGIC;  // (two roundings: no fma contraction)
+  const float q = qm - BC_RINT_MAGIC;
   float d = fmaf(q, -3.140625f, x);
   d = fmaf(q, -0.0009670257568359375f, d);
   d = fmaf(q, -6.2771141529083251953e-07f, d);
   d = fmaf(q, -1.2154201256553420762e-10f, d);
   const float s = d * d;
-  if (((int)q) & 1) d = -d;
   float u = 2.6083159809786593541503e-06f;
   u = fmaf(u, s, -0.0001981069071916863322258f);
   u = fmaf(u, s, 0.00833307858556509017944336f);
   u = fmaf(u, s, -0.166666597127914428710938f);
-  return fmaf(s, u * d, d);
+  const float r = fmaf(s, u * d, d);
+  return __uint_as_float(__float_as_uint(r) ^ (__float_as_uint(qm) << 31));
 }
 
 // SnakeBeta (vq/activations.py:107-118):  x + (1/(exp(b)+1e-9)) * sin(x*exp(a))^2.
@@ -67,20 +73,20 @@ __device__ __forceinline__ float snake(float x, float alpha_exp, float inv_beta)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
 __device__ __forceinline__ f32x2 bc_sin_pk(f32x2 x) {
-  const f32x2 t = x * splat2(0.318309886183790671538f);
-  const f32x2 q = {rintf(t.x), rintf(t.y)};
+  const f32x2 qm = x * splat2(0.318309886183790671538f) + splat2(BC_RINT_MAGIC);
+  const f32x2 q = qm - splat2(BC_RINT_MAGIC);
   f32x2 d = __builtin_elementwise_fma(q, splat2(-3.140625f), x);
   d = __builtin_elementwise_fma(q, splat2(-0.0009670257568359375f), d);
   d = __builtin_elementwise_fma(q, splat2(-6.2771141529083251953e-07f), d);
   d = __builtin_elementwise_fma(q, splat2(-1.2154201256553420762e-10f), d);
   const f32x2 s = d * d;
-  if (((int)q.x) & 1) d.x = -d.x;
-  if (((int)q.y) & 1) d.y = -d.y;
   f32x2 u = splat2(2.6083159809786593541503e-06f);
   u = __builtin_elementwise_fma(u, s, splat2(-0.0001981069071916863322258f));
   u = __builtin_elementwise_fma(u, s, splat2(0.00833307858556509017944336f));
   u = __builtin_elementwise_fma(u, s, splat2(-0.166666597127914428710938f));
   f32x2 r = __builtin_elementwise_fma(s, u * d, d);
+  r.x = __uint_as_float(__float_as_uint(r.x) ^ (__float_as_uint(qm.x) << 31));
+  r.y = __uint_as_float(__float_as_uint(r.y) ^ (__float_as_uint(qm.y) << 31));
   if (!(fabsf(x.x) < 39000.0f)) r.x = sinf(x.x);
   if (!(fabsf(x.y) < 39000.0f)) r.y = sinf(x.y);
   return r;

@@ -420,7 +420,7 @@ struct RSArgs {
 };
 
 __host__ __device__ constexpr size_t rs_lds_bytes(int D) {
-  return (size_t)RS_W7F + RS_W7T + 2 * (size_t)(RS_BN + 6 * D) * 96 + 2 * (size_t)RS_C * 6 * D * 4;
+  return (size_t)RS_W7F + RS_W7T + 2 * (size_t)(RS_BN + 6 * D) * (96 + 48) + 2 * (size_t)RS_C * 6 * D * 4;
 }
 
 template <int D>
@@ -428,16 +428,23 @@ __global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, Con
   constexpr int C = RS_C, NT = RS_NT;
   constexpr int HC = 6 * D;                 // halo columns shared by consecutive blocks
   constexpr int W = RS_BN + HC;             // input window columns of a block
-  constexpr int BPL = W * 96;               // bytes per input plane: full chunk [W][64 B], tail [W][32 B]
-  constexpr int TB = W * 64;
+  // Input planes, LINEAR layout (round 3): full chunk [W][96 B] (64 B of data), tail [W][48 B] (32 B): a column's
+  // fragment address is base + col * pitch, so every tap's address is the lane's base plus a constant (no per-tap
+  // swizzle arithmetic), and the pitches keep the fragment reads conflict-free at any column offset (ds_read_b128:
+  // 24 banks per column make each 16-lane group a permutation of the 16 four-bank slots; ds_read_b64: 12 banks).
+  constexpr int PF = 96, PT = 48;
+  constexpr int BPL = W * (PF + PT);        // bytes per input plane
+  constexpr int TB = W * PF;
   constexpr int HPL = RS_BN * 96, HTB = RS_BN * 64;  // h tile (aliases the input planes)
   constexpr int KH = (C * HC + RS_NTHR - 1) / RS_NTHR;       // halo samples per thread at a strip start
   constexpr int KI = (24 * HC + RS_NTHR - 1) / RS_NTHR;      // halo channel pairs per thread to split
   static_assert(RS_BN >= HC, "the next halo lies inside a block's new columns");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_rs[];
-  unsigned char* W7 = smem_rs;
-  unsigned char* PL = smem_rs + RS_W7F + RS_W7T;
+  // LDS: input planes first (every B-fragment address of a tap is then within a ds_read's 16-bit immediate offset
+  // of the lane's base), the two fp32 halo buffers, the k7 weights
+  unsigned char* PL = smem_rs;
   float* HL = reinterpret_cast<float*>(PL + 2 * BPL);  // 2 x [C][HC] activated fp32 halo
+  unsigned char* W7 = PL + 2 * BPL + 2 * C * HC * 4;
   __shared__ unsigned smx[2][RS_NW];
   __shared__ unsigned hmx[RS_NW];
   __shared__ float sisa[C], sisb[C];
@@ -485,18 +492,29 @@ __global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, Con
   // staging threads: channel pair sp (24), column lane cl: new columns HC + cl + 32 i of the window
   const int sp = tid >> 5, cl = tid & 31;
   float n0[4], n1[4], hv[KH];
+  // the thread's new-column offsets relative to the window start (interior blocks: + ws * 4 as the scalar offset)
+  const unsigned nof = (unsigned)((2 * sp * r.T + HC + cl) * 4);
   auto prefetch = [&](int w, int blk) {
     const int b = w / r.nstrip;
     const int ws = block_col(w, blk) - r.pl;  // clip column of window column 0
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(r.x + (long long)b * r.xbs), 0, C * r.T * 4, 0x00020000);
+    if (ws >= 0 && ws + W <= r.T) {  // interior window (uniform): no per-sample range checks
+      const int so = __builtin_amdgcn_readfirstlane(ws * 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = ws + HC + cl + 32 * i;
-      const bool ok = t >= 0 && t < r.T;
-      const unsigned o = ok ? (unsigned)((2 * sp * r.T + t) * 4) : 0xfffffff0u;
-      n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
-      n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? o + (unsigned)r.T * 4 : o, 0, 0));
+      for (int i = 0; i < 4; ++i) {
+        n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, nof + 128 * i, so, 0));
+        n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, nof + 128 * i + (unsigned)r.T * 4, so, 0));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = ws + HC + cl + 32 * i;
+        const bool ok = t >= 0 && t < r.T;
+        const unsigned o = ok ? (unsigned)((2 * sp * r.T + t) * 4) : 0xfffffff0u;
+        n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
+        n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ok ? o + (unsigned)r.T * 4 : o, 0, 0));
+      }
     }
     if (blk == 0) {  // a strip's first block also needs the halo (window columns [0, HC))
 #pragma unroll
@@ -588,17 +606,12 @@ __global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, Con
     }
     auto put = [&](int pr, int col, float v0, float v1) {  // channel pair pr at window column col
       unsigned h, l;
-      if (pr < 16) {
-        split2_h(v0 * sf, v1 * sf, h, l);
-        unsigned char* dst = PL + rr_bfull(col, pr >> 2) + (pr & 3) * 4;
-        *reinterpret_cast<unsigned*>(dst) = h;
-        *reinterpret_cast<unsigned*>(dst + BPL) = l;
-      } else {
-        split2_h(v0 * st, v1 * st, h, l);
-        unsigned char* dst = PL + TB + rr_btail(col, (pr - 16) >> 2) + ((pr - 16) & 3) * 4;
-        *reinterpret_cast<unsigned*>(dst) = h;
-        *reinterpret_cast<unsigned*>(dst + BPL) = l;
-      }
+      const bool full = pr < 16;
+      const float sc = full ? sf : st;
+      split2_h(v0 * sc, v1 * sc, h, l);
+      unsigned char* dst = PL + (full ? col * PF + 4 * pr : TB + col * PT + 4 * (pr - 16));
+      *reinterpret_cast<unsigned*>(dst) = h;
+      *reinterpret_cast<unsigned*>(dst + BPL) = l;
     };
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -641,18 +654,33 @@ __global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, Con
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = acct[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int col0 = g * 32 + lr;
+    // per-lane bases; tap t and n-tile j add the constants (t * D + 16 j) * pitch (uniform per tap)
+    const unsigned char* Bf = PL + col0 * PF + 16 * lg;
+    const unsigned char* Bt = PL + TB + col0 * PT + 8 * lg;
+    const unsigned char* Af = W7 + q * 1024 + lane * 16;
+    const unsigned char* At = W7 + RS_W7F + q * 512 + lane * 8;
 #pragma unroll 1
     for (int t = 0; t < 7; ++t) {
-      const f16x8_t a0 = *reinterpret_cast<const f16x8_t*>(W7 + ((t * 2 + 0) * 3 + q) * 1024 + lane * 16);
-      const f16x8_t a1 = *reinterpret_cast<const f16x8_t*>(W7 + ((t * 2 + 1) * 3 + q) * 1024 + lane * 16);
-      rr_taps(acc, PL, BPL, col0 + t * D, lg, a0, a1);
-      const f16x4_t at0 = *reinterpret_cast<const f16x4_t*>(W7 + RS_W7F + ((t * 2 + 0) * 3 + q) * 512 + lane * 8);
-      const f16x4_t at1 = *reinterpret_cast<const f16x4_t*>(W7 + RS_W7F + ((t * 2 + 1) * 3 + q) * 512 + lane * 8);
+      const f16x8_t a0 = *reinterpret_cast<const f16x8_t*>(Af + (t * 2 + 0) * 3072);
+      const f16x8_t a1 = *reinterpret_cast<const f16x8_t*>(Af + (t * 2 + 1) * 3072);
+      const unsigned char* bf = Bf + t * D * PF;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int off = rr_btail(col0 + 16 * j + t * D, lg >> 1) + 8 * (lg & 1);
-        const f16x4_t b0 = *reinterpret_cast<const f16x4_t*>(PL + TB + off);
-        const f16x4_t b1 = *reinterpret_cast<const f16x4_t*>(PL + BPL + TB + off);
+        const f16x8_t b0 = *reinterpret_cast<const f16x8_t*>(bf + 16 * j * PF);
+        const f16x8_t b1 = *reinterpret_cast<const f16x8_t*>(bf + 16 * j * PF + BPL);
+        floatx4 v = acc[j];
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0, v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, v, 0, 0, 0);
+        acc[j] = v;
+      }
+      const f16x4_t at0 = *reinterpret_cast<const f16x4_t*>(At + (t * 2 + 0) * 1536);
+      const f16x4_t at1 = *reinterpret_cast<const f16x4_t*>(At + (t * 2 + 1) * 1536);
+      const unsigned char* bt = Bt + t * D * PT;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const f16x4_t b0 = *reinterpret_cast<const f16x4_t*>(bt + 16 * j * PT);
+        const f16x4_t b1 = *reinterpret_cast<const f16x4_t*>(bt + 16 * j * PT + BPL);
         floatx4 v = acct[j];
         v = __builtin_amdgcn_mfma_f32_16x16x16f16(at1, b0, v, 0, 0, 0);
         v = __builtin_amdgcn_mfma_f32_16x16x16f16(at0, b1, v, 0, 0, 0);
