@@ -63,7 +63,7 @@ _SIGS = {
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 9  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 10  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -302,8 +302,8 @@ def precision_mode() -> int:
 
 
 def lstm_mode() -> int:
-    """Mode the ResLSTM packs and runs with (bc_reslstm_fwd maps bf16 to x6)."""
-    return 1 if _mode == 2 else _mode
+    """Mode the ResLSTM packs and runs with (bc_reslstm_fwd maps bf16 to h3: the recurrence stays fp32-class)."""
+    return 3 if _mode == 2 else _mode
 
 
 def precision_name() -> str:

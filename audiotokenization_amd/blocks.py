@@ -86,9 +86,9 @@ class ResidualUnit(nn.Module):
         return self.block[0]
 
     def _fused_cfg(self):
-        """cfg of the one-launch unit (bc_resunit_fwd), or -1 (x6 / h3 mode, no anti-aliasing, C fits)."""
+        """cfg of the one-launch unit (bc_resunit_fwd), or -1 (x6 / bf16 / h3 mode, no anti-aliasing, C fits)."""
         mode = L.precision_mode()
-        if mode not in (1, 3) or self.block[2].antialias:
+        if mode not in (1, 2, 3) or self.block[2].antialias:
             return -1
         conv7 = _conv_of(self.block[1])
         return L.load().bc_resunit_select_cfg(conv7.in_channels, conv7.dilation, mode)

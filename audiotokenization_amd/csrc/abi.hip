@@ -77,7 +77,7 @@ int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packe
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
-  if (cfg != resunit_select_cfg(C, dilation, 1) && cfg != resunit_select_cfg(C, dilation, 3)) return BC_ERR_ARG;
+  if (cfg != resunit_select_cfg(C, dilation, cfg / 100)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   return resunit_launch(x_raw, x_act, w7_packed, b7, mid_snake_alpha_exp, mid_snake_inv_beta, w1_packed, b1,
                         out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, C, T, dilation, pad_left, cfg,
@@ -95,7 +95,7 @@ int bc_resunit_fwd_snake_in(const float* x_raw, const float* in_snake_alpha_exp,
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
-  if (cfg != resunit_select_cfg(C, dilation, 1) && cfg != resunit_select_cfg(C, dilation, 3)) return BC_ERR_ARG;
+  if (cfg != resunit_select_cfg(C, dilation, cfg / 100)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   return resunit_launch(x_raw, x_raw, w7_packed, b7, mid_snake_alpha_exp, mid_snake_inv_beta, w1_packed, b1,
                         out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, C, T, dilation, pad_left, cfg,
@@ -177,14 +177,19 @@ int bc_aa_snake_fwd(const float* x, const float* snake_alpha_exp, const float* s
                          S(stream));
 }
 
-// The recurrence is accuracy-critical: mode 2 (bf16 conv products) keeps the LSTM fp32-accurate.
+// The recurrence is accuracy-critical: mode 2 (bf16 conv products) keeps the LSTM fp32-class, on the h3
+// arithmetic since round 3 (x6 before: the same accuracy class at ~2.8x the recurrence time).
 // Mode 3 (h3) runs the input projection as an h3 conv and the recurrence as the h3 persistent kernel.
-static int lstm_mode(int mode) { return mode == 2 ? 1 : mode; }
-static bool lstm_use_seq(int H, int mode) { return (lstm_mode(mode) == 1 || mode == 3) && lstm_seq_ok(H); }
+static int lstm_mode(int mode) { return mode == 2 ? 3 : mode; }
+static bool lstm_use_seq(int H, int mode) {
+  const int m = lstm_mode(mode);
+  return (m == 1 || m == 3) && lstm_seq_ok(H);
+}
+static int lstm_planes(int mode) { return lstm_mode(mode) == 3 ? 2 : 3; }
 
 long long bc_lstm_hh_packed_floats(int H, int mode) {
   if (H <= 0 || H % 16 || mode < 0 || mode > 3) return -1;
-  if (lstm_use_seq(H, mode)) return lstm_seq_packed_bytes(H, mode == 3 ? 2 : 3) / 4;
+  if (lstm_use_seq(H, mode)) return lstm_seq_packed_bytes(H, lstm_planes(mode)) / 4;
   return (long long)4 * H * H;
 }
 
@@ -195,7 +200,7 @@ int bc_mfma_probe(float* out, int nwg, int iters, void* stream) { return mfma_pr
 int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode) {
   if (!w_hh_host || !packed_host || H <= 0 || H % 16 || mode < 0 || mode > 3) return BC_ERR_ARG;
   if (lstm_use_seq(H, mode))
-    lstm_seq_pack(w_hh_host, reinterpret_cast<unsigned short*>(packed_host), H, mode == 3 ? 2 : 3);  // persistent kernel
+    lstm_seq_pack(w_hh_host, reinterpret_cast<unsigned short*>(packed_host), H, lstm_planes(mode));  // persistent kernel
   else if (lstm_fast_ok(H))
     lstm_pack_hh2(w_hh_host, packed_host, H);  // layout of the register-resident fast step kernel
   else
@@ -257,7 +262,7 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   int rc = conv_launch(a, 1, conv_select_cfg(4 * H, Cin, 1, 1, 1, mode), st);
   if (rc) return rc;
   if (lstm_use_seq(H, mode))  // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
-    return lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(whh), lout, cst, H, T, B, mode == 3 ? 2 : 3, st,
+    return lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(whh), lout, cst, H, T, B, lstm_planes(mode), st,
                            h0, c0, hT, cT, call_status);
   if (h0 || c0 || hT || cT) return BC_ERR_UNSUPPORTED;  // carried state: the persistent kernel only
   const bool fast = lstm_fast_ok(H);

@@ -17,7 +17,9 @@
 //            (Bs + As): a 96 x 128 tile fits in 80 KiB, i.e. two workgroups per CU.
 // Same weight packing as bc_conv1d_pack for the unit's cfg (M = C in a single m-group).
 // P = 3: x6 (3 bf16 planes, 6 products); P = 2: h3 (2 block-scaled fp16 planes, 3 products; the k=7
-// input is scaled per staged chunk as in conv1d_x6.hip, h per workgroup tile from its block maximum).
+// input is scaled per staged chunk as in conv1d_x6.hip, h per workgroup tile from its block maximum);
+// P = 1: bf16 (one plane, one product: the bf16 precision mode, x and h rounded to bf16 like the lone
+// bf16 convs round their inputs).
 #include <cstdio>
 #include <cstdlib>
 
@@ -48,7 +50,7 @@ __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ 
 // TPS: k=7 taps per phase-1 K-step (one A copy, one wait and one barrier per TPS taps).
 template <int MT, int NT, int WM, int WN, int P, int TPS = 1>
 __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
-  static_assert(P == 2 || P == 3, "x6 or h3 operands");
+  static_assert(P >= 1 && P <= 3, "bf16, h3 or x6 operands");
   typedef typename FragType<P>::type frag_t;
   __shared__ unsigned smax[2][8];  // P == 2: per-wave block maxima (k=7 input chunks by parity; h tile)
   constexpr int BN = 16 * NT * WN;
@@ -165,6 +167,10 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
           *reinterpret_cast<unsigned*>(p + bplane) = m;
           continue;
         }
+        if constexpr (P == 1) {
+          *reinterpret_cast<unsigned*>(Bs + bgrp(col, bp >> 2) + (bp & 3) * 4) = pk_bf16(bv0[i], bv1[i]);
+          continue;
+        }
         unsigned h, m, l;
         split2(bv0[i], bv1[i], h, m, l);
         unsigned char* p = Bs + bgrp(col, bp >> 2) + (bp & 3) * 4;
@@ -249,6 +255,9 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
             acc[i][j] = t;
           }
           continue;
+        } else if constexpr (P == 1) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], acc[i][j], 0, 0, 0);
         } else {
         const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(Aq + QA * 1024);
         const bf16x8_t a2 = *reinterpret_cast<const bf16x8_t*>(Aq + 2 * QA * 1024);
@@ -372,6 +381,10 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
       const f32x2 hi = snake_pk((f32x2){acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]}, (f32x2){sa[2], sa[3]},
                                 (f32x2){sb[2], sb[3]});
       v[0] = lo.x, v[1] = lo.y, v[2] = hi.x, v[3] = hi.y;
+      if constexpr (P == 1) {
+        *reinterpret_cast<u32x2_t*>(hrow + hs_off(n, g)) = (u32x2_t){pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
+        continue;
+      }
       unsigned h0, m0, l0, h1, m1, l1;
       split2(v[0], v[1], h0, m0, l0);
       split2(v[2], v[3], h1, m1, l1);
@@ -407,6 +420,8 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
           t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0], w1f[kc][0], t, 0, 0, 0);
           acc2[0][j] = t;
           continue;
+        } else if constexpr (P == 1) {
+          acc2[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][0], t, 0, 0, 0);
         } else {
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[0], w1f[kc][2], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[1], w1f[kc][1], t, 0, 0, 0);
@@ -463,7 +478,7 @@ static int ru_tps(const X6Tile& t, int C, int d, int P) {
     const char* e = getenv("BC_RU_TPS");
     return e ? atoi(e) : 0;
   }();
-  if (P != 2) return 1;
+  if (P == 3) return 1;
   if (forced == 1 || forced == 2 || forced == 4) return forced;
   int bp, hp;
   for (int tps : {4, 2})
@@ -471,10 +486,10 @@ static int ru_tps(const X6Tile& t, int C, int d, int P) {
   return 1;
 }
 
-// mode 1 (x6) -> cfg 1xx, mode 3 (h3) -> cfg 3xx (same tile table)
+// mode 1 (x6) -> cfg 1xx, mode 2 (bf16) -> cfg 2xx, mode 3 (h3) -> cfg 3xx (same tile table)
 int resunit_select_cfg(int C, int d, int mode) {
-  if ((mode != 1 && mode != 3) || C < 16 || C % 16 || d <= 0) return -1;
-  const int P = mode == 3 ? 2 : 3;
+  if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
+  const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
   for (int cfg : kRUCandidates) {
     const X6Tile& t = x6_tile(cfg);
@@ -483,7 +498,7 @@ int resunit_select_cfg(int C, int d, int mode) {
     int bp, hp;
     const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
     if (forced ? (cfg != forced || lds > 160 * 1024) : lds > RU_LDS_MAX) continue;
-    return cfg + (P == 2 ? 200 : 0);
+    return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
   }
   return -1;
 }
@@ -515,10 +530,10 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
     e.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(r.w1) +
                                            (long long)r.nck1 * P * QA * 1024);
   }
-  if (P == 2 && tps == 4)
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P == 2 ? 4 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
-  else if (P == 2 && tps == 2)
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P == 2 ? 2 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  if (P != 3 && tps == 4)
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 4 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+  else if (P != 3 && tps == 2)
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 2 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
   else
     hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
   BC_CHECK_LAUNCH();
@@ -526,12 +541,13 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 }
 
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
-  const bool h3 = cfg >= 300 && cfg < 400;
-  if (!(h3 || (cfg >= 100 && cfg < 200)) || cfg != resunit_select_cfg(C, d, h3 ? 3 : 1)) return -1;
-  if (h3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
+  const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
+  if (mode < 1 || mode > 3 || cfg != resunit_select_cfg(C, d, mode)) return -1;
+  if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
-  return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, h3 ? 2 : 3,
-                  ru_tps(t, C, d, h3 ? 2 : 3));
+  const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
+  return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, P,
+                  ru_tps(t, C, d, P));
 }
 
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
@@ -561,6 +577,7 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
   if (isa) a.x = x_raw;  // snake on load
 #define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
   case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \
+  case 200 + ID: return launch_ru<MT, NT, WM, WN, 1>(a, e, r, B, st); \
   case 300 + ID: return launch_ru<MT, NT, WM, WN, 2>(a, e, r, B, st);
   switch (cfg) {
     BC_RU_CASES(11, 3, 1, 1, 8)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 9
+#define BC_ABI_VERSION 10
 
 int bc_abi_version(void);
 
@@ -44,7 +44,8 @@ int bc_abi_version(void);
  * shapes where it applies (Cin >= 16), else the fp32 kernel.  Its error against fp64 is at or below
  * the fp32 kernel's.  mode 2: plain bf16 products with fp32 accumulation (one MFMA
  * per pair; BASELINE config 5's "bf16 encoder conv stack"; activations stay fp32 in memory) where
- * Cin >= 16, else fp32.  bc_reslstm_fwd runs mode 2 as mode 1 (the recurrence stays fp32-accurate).
+ * Cin >= 16, else fp32.  bc_reslstm_fwd runs mode 2 as mode 3 (the recurrence stays fp32-class; its
+ * input projection is packed with cfg = bc_conv1d_select_cfg(..., 3)).
  * mode 3 ("h3", the package default): fp32-class block-scaled 2 x fp16 split — each operand block is
  * scaled by a power of two from its maximum (weights per output row, packed by bc_conv1d_pack;
  * activations per staged 32-channel chunk) and split v*S = hi + lo (two fp16 terms, 22 significant
@@ -62,14 +63,14 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
                   int K, int stride, int dilation, int pad_left, int epilogue, int cfg,
                   void* stream);
 
-/* ---- ResidualUnit in one launch (modes 1 "x6" and 3 "h3"; C in {16, 32, 48, 64, 96}) -------------
+/* ---- ResidualUnit in one launch (modes 1 "x6", 2 bf16 and 3 "h3"; C in {16, 32, 48, 64, 96}) -------
  * Replaces ResidualUnit.forward (vq/module.py:88-89) after its first Activation1d:
  *   v = x_raw + conv1(snake_mid(conv7_d(x_act)))      (x_act = snake1(x_raw), from the producer)
  *   y = v, or snake_out(v), or y = v and y2 = snake_out(v)  (epilogue as bc_conv1d_fwd)
  * x_raw, x_act, y, y2: [B][C][T]; the k=7 conv keeps length T (pad_left = 3*dilation non-causal,
  * 6*dilation causal; the rest on the right).  w7_packed / w1_packed = bc_conv1d_pack(folded weight,
  * K = 7 / 1, cfg) with cfg = bc_resunit_select_cfg(C, dilation, mode); that returns -1 where the
- * unit does not fit one workgroup, or mode is 0 / 2 (then run the two bc_conv1d_fwd calls).  The
+ * unit does not fit one workgroup, or mode is 0 (then run the two bc_conv1d_fwd calls).  The
  * activated k=7 output stays in LDS (never written to memory).  mid_snake_*: the unit's second
  * Activation1d. */
 int bc_resunit_select_cfg(int C, int dilation, int mode);
@@ -144,7 +145,7 @@ int bc_tanh_fwd(const float* x, float* y, long long n, void* stream);
  * pointer arrays are HOST arrays of device pointers.  out = snake(y + x) when out_snake_alpha_exp !=
  * NULL (the Activation1d that follows the ResLSTM in both stacks), else y + x.  workspace:
  * bc_lstm_workspace_floats(B, H, T) device floats.  H % 16 == 0.
- * Modes 1 and 3 with H in {256, 512, 1024, 1536}: the recurrence runs as ONE persistent launch per
+ * Modes 1, 2 (= 3) and 3 with H in {256, 512, 1024, 1536}: the recurrence runs as ONE persistent launch per
  * layer (H/8 workgroups that must all be resident at once — checked against the kernel's occupancy,
  * else 3 — W_hh register-resident; mode 1 3xbf16-split, mode 3 2xfp16-split MFMA); otherwise one
  * launch per step (fp32 MFMA).

@@ -354,6 +354,46 @@ def test_resunit_fused(dev, C, d, causal, B, T, ru_prec):
     assert torch.equal(lraw.cpu(), got) and torch.equal(lact.cpu(), act.cpu())
 
 
+@pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, True, 1, 24000), (96, 3, False, 2, 513),
+                                           (96, 9, False, 1, 4096), (64, 1, True, 2, 300), (16, 3, False, 3, 257)])
+def test_resunit_fused_bf16(dev, C, d, causal, B, T):
+    """Precision 'bf16' (config 5) runs the ResidualUnit in one launch too (resunit_x6_kernel<..., P = 1>):
+    the k=7 input and the activated h rounded to bf16 as the lone bf16 convs round their inputs, fp32
+    accumulation.  Against the two-launch bf16 path: the same roundings and the same accumulation
+    order, so agreement to a few fp32 ulps; against the fp32 oracle: bf16-rounding sized."""
+    from audiotokenization_amd.blocks import produce_conv
+
+    old = L.precision_mode()
+    L.set_precision("bf16")
+    try:
+        g = torch.Generator().manual_seed(C * 10 + d + 7)
+        ru = BL.ResidualUnit(C, dilation=d, causal=causal)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            ru.block[k].act.load_state_dict(_snake(C, g).state_dict())
+        x = torch.randn(B, C, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        want = O.residual_unit(x, sd, "", d, causal, False)
+        ru.to(dev)
+        cfg = ru._fused_cfg()
+        assert 200 <= cfg < 300, cfg
+        assert "resunit_x6_kernel" in L.resunit_kernel_name(cfg, C, d) and ", 1, " in L.resunit_kernel_name(cfg, C, d)
+        xd = x.to(dev)
+        xa = ru.first_act(xd)
+        got = ru.flow(xd, xa)[0].cpu()
+        lazy = ru.flow(xd, None)[0].cpu()
+        _, h = produce_conv(ru.block[1], xa, None, want_raw=False, next_act=ru.block[2])
+        two = produce_conv(ru.block[3], h, residual=xd, want_raw=True, next_act=None)[0].cpu()
+    finally:
+        L._mode = old
+    assert torch.equal(lazy, got)
+    assert_close_rel(got, two, 1e-5, f"bf16 resunit C={C} d={d}: one launch vs two")
+    assert_close_rel(got, want, 2e-2, f"bf16 resunit C={C} d={d} vs fp32 oracle")
+    rel = ((got - want).abs().max() / want.abs().max()).item()
+    assert rel > 1e-5, rel  # really bf16 products
+
+
 @pytest.mark.parametrize("d,B,T", [(3, 1, 1001), (3, 1, 4096), (1, 1, 24000), (9, 1, 24000), (3, 2, 700),
                                    (2, 1, 1001), (4, 1, 1001), (5, 1, 1001), (9, 2, 129), (1, 3, 128), (3, 1, 5)])
 def test_resunit_c48_h3_sweep(dev, d, B, T):
