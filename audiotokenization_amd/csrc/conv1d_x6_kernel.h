@@ -37,7 +37,7 @@ namespace bc {
 // ever decreases within a workgroup, the accumulator is rescaled (exactly) when it does, and the
 // epilogue multiplies by 1 / (x scale * per-row weight scale).
 // PW: pointwise (K = 1, the input tile is exactly BN columns) with the two-chunk-deep B prefetch.
-// TPS: taps per K-step of the multi-tap path (1 or 2): one A copy, one wait and one barrier cover
+// TPS: taps per K-step of the multi-tap path (1, 2, or 4 for bf16 on the 16-wave tile): one A copy, one wait and one barrier cover
 // TPS (chunk, tap) units, i.e. BK = 32 * TPS per barrier.
 // DB (multi-tap path, kst >= 3 for P == 2, >= 2 otherwise): two B buffers; chunk c + 1 is staged into the
 // idle one during chunk c's K-steps (maxima published at step 1, split and stored at step 2 for h3 /
@@ -450,6 +450,15 @@ inline bool x6_db_on() {
   return v;
 }
 
+// BC_X6_TPS4=0 keeps the bf16 16-wave tile at two taps per K-step (A/B timing).
+inline bool x6_tps4_on() {
+  static const bool v = [] {
+    const char* e = getenv("BC_X6_TPS4");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 struct X6Variant {
   bool pw;
   int tps;
@@ -467,6 +476,10 @@ inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
   // one tap per step fits (256 x 256: k7 768 -4.5 %, k3 1536 -6 %); NT == 1 tiles never (slower, spills)
   const bool db = x6_db_on() && P <= 2 && t.NT > 1;
   const bool tps2 = P <= 2 && K > 1 && x6_tps() == 2;
+  // bf16 on the 16-wave tile: one product per pair makes a two-tap K-step a third of h3's, too short to hide
+  // the next step's A copy and the barrier; four taps per K-step over the double B buffer (k7: 2 K-steps per chunk)
+  if (P == 1 && t.WM * t.WN == 16 && db && tps2 && x6_tps4_on() && (K + 3) / 4 >= min_kst && fits(4, 2))
+    return {false, 4, true, x6_lds(t, ncol, P, s, 4, 2)};
   if (db && tps2 && (K + 1) / 2 >= min_kst && fits(2, 2)) return {false, 2, true, x6_lds(t, ncol, P, s, 2, 2)};
   if (tps2 && fits(2, 1)) return {false, 2, false, x6_lds(t, ncol, P, s, 2)};
   if (db && K >= min_kst && fits(1, 2)) return {false, 1, true, x6_lds(t, ncol, P, s, 1, 2)};
@@ -498,6 +511,13 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   const X6Variant v = x6_variant(t, P, a.K, a.s, a.d);
   constexpr int T2 = P <= 2 ? 2 : 1;
   constexpr bool D2 = P <= 2;
+  if constexpr (P == 1 && WM * WN == 16) {
+    if (v.tps == 4) {
+      hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 4, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
+      BC_CHECK_LAUNCH();
+      return BC_OK;
+    }
+  }
   if (v.pw)
     hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
   else if (v.db && v.tps == 2)

@@ -64,7 +64,7 @@ def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
     planes = targs[4] if kname.startswith(("conv1d_x6_kernel", "resunit_x6_kernel")) and len(targs) >= 5 else None
-    if kname.startswith("resunit_rr_kernel"):  # resunit_rr.hip: h3 (two fp16 planes) only
+    if kname.startswith(("resunit_rr_kernel", "resunit_strip_kernel")):  # resunit_rr.hip: h3 (two fp16 planes) only
         planes = "2"
     if planes == "1":
         return BF16_MFMA_PEAK_TFLOPS, 1, "bf16 products (precision 'bf16'): dense BF16 MFMA peak"

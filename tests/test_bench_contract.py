@@ -1,0 +1,20 @@
+"""bench.py's roofline bookkeeping (CPU): every kernel the encoder launches is priced against the MFMA
+ceiling of the arithmetic it runs (h3: dense FP16 / 3, x6: dense BF16 / 6, bf16: dense BF16)."""
+import bench
+
+
+def test_kernel_peak_by_operand_planes():
+    bf16, h3, x6 = bench.BF16_MFMA_PEAK_TFLOPS, bench.BF16_MFMA_PEAK_TFLOPS / 3, bench.BF16_MFMA_PEAK_TFLOPS / 6
+    cases = {
+        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>": h3,
+        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true>": bf16,
+        "conv1d_x6_kernel<6, 1, 1, 8, 3, false, 1, false>": x6,
+        "resunit_x6_kernel<6, 1, 1, 8, 2, 2>": h3,
+        "resunit_x6_kernel<6, 1, 1, 8, 1, 2>": bf16,
+        "resunit_rr_kernel<96, 2, 1>": h3,
+        "resunit_strip_kernel<3>": h3,
+        "conv1d_mfma_kernel<3, 1, 4, 4, 4>": bench.FP32_MFMA_PEAK_TFLOPS,
+    }
+    for name, peak in cases.items():
+        got = bench.kernel_peak(name)[0]
+        assert abs(got - peak) < 1e-9, (name, got, peak)
