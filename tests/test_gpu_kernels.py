@@ -133,6 +133,46 @@ def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
         L._mode = old
 
 
+@pytest.mark.parametrize("Cin,Cout,d,B,T,cfgs", [(192, 192, 3, 2, 70000, (322, 320)), (384, 384, 9, 3, 24000, (322, 320)),
+                                             (768, 768, 9, 3, 8000, (322, 321)), (192, 192, 1, 2, 70000, (222, 220))])
+def test_k7_tiles_large(dev, Cin, Cout, d, B, T, cfgs):
+    """k7 convs at encoder scale (hundreds of tiles, several per CU): two tiles (16 waves and 8 waves, each a
+    different grid and tile walk) agree bit for bit, and the output matches the fp64 oracle in windows at the
+    start, across tile boundaries and at the end."""
+    prec = "bf16" if cfgs[0] < 300 else "h3"
+    old = L.precision_mode()
+    L.set_precision(prec)
+    try:
+        g = torch.Generator().manual_seed(Cin + d * 7 + T)
+        K, pad = 7, 3 * d
+        m = CV.WNConv1d(Cin, Cout, kernel_size=K, dilation=d, padding=pad)
+        conv = _rand_wn_conv(m, g)
+        x = torch.randn(B, Cin, T, generator=g)
+        sd = {k: v.detach() for k, v in conv.state_dict().items()}
+        m.to(dev)
+        xd = x.to(dev)
+        st = torch.cuda.current_stream().cuda_stream
+        outs = {}
+        for cfg in cfgs:
+            wp, bias = m.packed_as(cfg, dev)
+            y = torch.empty(B, Cout, T, device=dev)
+            L.call("bc_conv1d_fwd", xd.data_ptr(), wp.data_ptr(), L.ptr(bias), 0, 0, 0, y.data_ptr(), 0,
+                   B, Cin, T, Cout, T, K, 1, d, pad, 0, cfg, st)
+            torch.cuda.synchronize()
+            outs[cfg] = y.cpu()
+    finally:
+        L._mode = old
+    assert torch.equal(outs[cfgs[0]], outs[cfgs[1]]), (outs[cfgs[0]] - outs[cfgs[1]]).abs().max()
+    got = outs[cfgs[0]]
+    tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if prec == "h3" else 2e-2
+    xp = torch.nn.functional.pad(x.double(), (pad, pad))
+    sd64 = {k: v.double() for k, v in sd.items()}
+    W = 300
+    for s0 in (0, 250, T // 2 - 7, T - W):
+        want = O.conv(xp[..., s0:s0 + W + 6 * d], sd64, "", K, 1, 0, d, False)
+        assert_close_rel(got[..., s0:s0 + W].double(), want, tol, f"{prec} cfg {cfgs[0]} window {s0}")
+
+
 CONVT_CASES = [
     # Cin, Cout, stride, causal, snake, B, T
     (64, 32, 2, False, True, 2, 301),
