@@ -266,8 +266,17 @@ def test_kernel_names_come_from_the_launchers():
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3) == \
         "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>"
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 3), 3).endswith("false, 1, true>")
-    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_rr_kernel<48, 4, 1>"
+    # bf16 on the 16-wave tile: four taps per K-step over the double B buffer
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(384, 384, 7, 1, 3, 2), 7, 1, 3) == \
+        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true>"
+    # C = 48 in h3: the streaming strip kernel (one per dilation); C = 96: the one-launch x6-family unit
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_strip_kernel<1>"
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 9, 3), 48, 9) == "resunit_strip_kernel<9>"
     n96 = L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 3), 96, 3)
     assert n96.startswith("resunit_x6_kernel<") and ", 2, " in n96, n96
+    # bf16: the same unit with one bf16 plane (P = 1), at C = 48 too
+    for C, d in ((48, 1), (96, 3)):
+        nb = L.resunit_kernel_name(lib.bc_resunit_select_cfg(C, d, 2), C, d)
+        assert nb.startswith("resunit_x6_kernel<") and re.search(r", 1, [124]>$", nb), nb
     with pytest.raises(L.BigCodecLibraryError):
         L.conv_kernel_name(12345, 7)

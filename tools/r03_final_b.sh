@@ -1,0 +1,14 @@
+#!/bin/bash
+# End-of-round regression, part B (after round_final_a.sh): rocprofv3 kernel stats of the default bench, configs 3-6,
+# the PMC passes (traffic + MFMA busy per kernel).  Every GPU step has its own time limit; the first failure ends it.
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out/final gpurun_out/stats
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats -o run -- \
+  python3 bench.py --no-cpu-baseline --no-x6 > gpurun_out/stats/bench.log 2>&1 || { echo "stats run failed $?"; exit 1; }
+for c in 3 4 5 6; do
+  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline --no-x6 > gpurun_out/final/bench_config$c.json 2> gpurun_out/final/bench_config$c.err || { echo "config $c failed $?"; exit 1; }
+done
+PMC_TIMEOUT=300 bash tools/gpu_pmc.sh || { echo "pmc failed $?"; exit 1; }
+grep -m1 "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>" gpurun_out/stats/run_kernel_stats.csv
+echo done
