@@ -77,7 +77,7 @@ int bc_resunit_fwd(const float* x_raw, const float* x_act, const float* w7_packe
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
-  if (cfg != resunit_select_cfg(C, dilation, cfg / 100)) return BC_ERR_ARG;
+  if (!resunit_cfg_ok(cfg, C, dilation)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   return resunit_launch(x_raw, x_act, w7_packed, b7, mid_snake_alpha_exp, mid_snake_inv_beta, w1_packed, b1,
                         out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, C, T, dilation, pad_left, cfg,
@@ -95,7 +95,7 @@ int bc_resunit_fwd_snake_in(const float* x_raw, const float* in_snake_alpha_exp,
     return BC_ERR_ARG;
   if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
   if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
-  if (cfg != resunit_select_cfg(C, dilation, cfg / 100)) return BC_ERR_ARG;
+  if (!resunit_cfg_ok(cfg, C, dilation)) return BC_ERR_ARG;
   if (B == 0 || T == 0) return BC_OK;
   return resunit_launch(x_raw, x_raw, w7_packed, b7, mid_snake_alpha_exp, mid_snake_inv_beta, w1_packed, b1,
                         out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, C, T, dilation, pad_left, cfg,

@@ -48,6 +48,7 @@ void conv_pack_weight(const float* w, float* out, int Cout, int Cin, int K, int 
 int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
 
 int resunit_select_cfg(int C, int d, int mode);
+bool resunit_cfg_ok(int cfg, int C, int d);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,

@@ -411,6 +411,9 @@ inline constexpr X6Tile kX6Tiles[] = {
     {6, 4, 2, 4},  // 120: BM=192 BN=256  (h3: 96 x 64 per wave)
     {8, 4, 2, 4},  // 121: BM=256 BN=256
     {6, 2, 2, 8},  // 122: BM=192 BN=256, 16 waves of 96 x 32 (h3 and bf16)
+    // one-launch ResidualUnit only (resunit_x6.hip; the conv kernel does not instantiate them):
+    {3, 2, 2, 4},  // 123: BM=96  BN=128, 48 x 32 per wave (C = 96: 10 instead of 14 LDS fragment reads per K32)
+    {3, 4, 1, 8},  // 124: BM=48  BN=512, 48 x 64 per wave (bf16 C = 48: 7 reads per 12 MFMAs instead of 4 per 3)
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -574,6 +577,8 @@ int x6_launch_tile(ConvArgs& a, int B, int tile, hipStream_t st);
     case 20: return launch_x6<6, 4, 2, 4, P>(a, B, st);            \
     case 21: return launch_x6<8, 4, 2, 4, P>(a, B, st);            \
     case 22: return launch_x6_w16<P>(a, B, st);                    \
+    case 23:                                                       \
+    case 24: return BC_ERR_UNSUPPORTED;                            \
   }                                                                \
   return BC_ERR_ARG;
 

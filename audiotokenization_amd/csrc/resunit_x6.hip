@@ -47,9 +47,16 @@ struct RUExtra {
 
 __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
+// Minimum waves per SIMD the unit is compiled for: 4 (<= 128 VGPRs, two workgroups per CU) for the NT = 1
+// tiles and the 48 x 32-per-wave C = 96 tile (123); 2 otherwise (the 48 x 512 tile 124 spills 234 VGPRs at 128:
+// its phase 2 holds 16 n-tiles per wave).
+constexpr int ru_min_waves(int MT, int NT, int WM, int P) {
+  return (NT == 1 || (MT == 3 && NT == 2 && WM == 2)) ? 4 : 2;
+}
+
 // TPS: k=7 taps per phase-1 K-step (one A copy, one wait and one barrier per TPS taps).
 template <int MT, int NT, int WM, int WN, int P, int TPS = 1>
-__global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
+__global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
   static_assert(P >= 1 && P <= 3, "bf16, h3 or x6 operands");
   typedef typename FragType<P>::type frag_t;
   __shared__ unsigned smax[2][8];  // P == 2: per-wave block maxima (k=7 input chunks by parity; h tile)
@@ -450,7 +457,12 @@ __global__ void __launch_bounds__(512, (NT == 1 ? 4 : 2)) resunit_x6_kernel(Conv
 // MI355X, the one-launch unit only beats the two separate convs when a second workgroup's MFMAs hide
 // each workgroup's operand loads and epilogue stores (at one workgroup per CU it was a wash at C = 48
 // and 96 and 8% slower at C = 192, profiles/r01_x6b_layer_profile.txt vs r01_resunit_v1_layers.txt).
-static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105};
+// h3 / bf16 at C = 96 take 123 first (the same 96 x 128 tile as 2 x 4 waves of 48 x 32: 10 instead of 14 LDS
+// fragment reads per K32 unit, bit-identical outputs): 4-6 % per unit (profiles/r03m_ru_tiles.txt); x6 is
+// neutral there (7.05 vs 7.08 ms) and keeps 109.  The 48-row bf16 tiles with more columns per wave (106, 124)
+// need more than 128 VGPRs (one workgroup per CU) and run 1.8-2.1x slower than 111.
+static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 123, 124};
+static const int kRUCandidatesP12[] = {123, 109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 124};
 constexpr size_t RU_LDS_MAX = 80 * 1024;
 // BC_RU_CFG forces one candidate tile (timing experiments; it must fit the 160 KiB of a CU).
 static int ru_forced_cfg() {
@@ -491,7 +503,7 @@ int resunit_select_cfg(int C, int d, int mode) {
   if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
-  for (int cfg : kRUCandidates) {
+  for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
     if (d > RU_MAX_DIL) return -1;
@@ -501,6 +513,22 @@ int resunit_select_cfg(int C, int d, int mode) {
     return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
   }
   return -1;
+}
+
+// cfg is a one-launch unit tile for (C, d) in its mode: the selected one, or another candidate whose 16 * MT * WM
+// rows cover C and whose LDS fits a CU (A/B timing and the tile bit-identity tests pick tiles explicitly).
+bool resunit_cfg_ok(int cfg, int C, int d) {
+  const int mode = cfg / 100;
+  if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0 || d > RU_MAX_DIL) return false;
+  if (cfg == resunit_select_cfg(C, d, mode)) return true;
+  const int base = cfg % 100 + 100;
+  bool cand = false;
+  for (int c : kRUCandidates) cand = cand || c == base;
+  if (!cand) return false;
+  const X6Tile& t = x6_tile(base);
+  const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
+  int bp, hp;
+  return x6_BM(t) == C && ru_lds(t, C, d, P, &bp, &hp, ru_tps(t, C, d, P)) <= 160 * 1024;
 }
 
 template <int MT, int NT, int WM, int WN, int P>
@@ -542,7 +570,7 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
-  if (mode < 1 || mode > 3 || cfg != resunit_select_cfg(C, d, mode)) return -1;
+  if (mode < 1 || mode > 3 || !resunit_cfg_ok(cfg, C, d)) return -1;
   if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
@@ -590,6 +618,8 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
     BC_RU_CASES(4, 6, 2, 1, 8)
     BC_RU_CASES(5, 4, 2, 1, 8)
     BC_RU_CASES(17, 4, 1, 2, 4)
+    BC_RU_CASES(23, 3, 2, 2, 4)
+    BC_RU_CASES(24, 3, 4, 1, 8)
   }
 #undef BC_RU_CASES
   return BC_ERR_ARG;

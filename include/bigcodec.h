@@ -70,7 +70,9 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
  * x_raw, x_act, y, y2: [B][C][T]; the k=7 conv keeps length T (pad_left = 3*dilation non-causal,
  * 6*dilation causal; the rest on the right).  w7_packed / w1_packed = bc_conv1d_pack(folded weight,
  * K = 7 / 1, cfg) with cfg = bc_resunit_select_cfg(C, dilation, mode); that returns -1 where the
- * unit does not fit one workgroup, or mode is 0 (then run the two bc_conv1d_fwd calls).  The
+ * unit does not fit one workgroup, or mode is 0 (then run the two bc_conv1d_fwd calls).  Another
+ * candidate tile of the same mode whose rows cover C is accepted too (same results, A/B timing); any
+ * other cfg returns BC_ERR_ARG.  The
  * activated k=7 output stays in LDS (never written to memory).  mid_snake_*: the unit's second
  * Activation1d. */
 int bc_resunit_select_cfg(int C, int dilation, int mode);

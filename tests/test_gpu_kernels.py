@@ -288,6 +288,42 @@ def test_reslstm(dev, H, layers, B, T, prec):
     assert L.load().bc_lstm_status(1) == 0
 
 
+@pytest.mark.parametrize("lprec", ["h3", "x6"])
+def test_reslstm_half_split_bit_identical(dev, lprec):
+    """The persistent recurrence runs a launch of <= 32 clips as two halves of 16 (NTH = 1) and a launch of 33-64
+    clips as two halves of 32: a clip's gates are summed over the same K ranges, waves and MFMA chains either way,
+    so in x6 (exact per-element operand splits everywhere) the first 32 / 20 clips of a 64-clip batch come out
+    bit-identical when run alone.  In h3 the input projection's block scales span the clips of a column tile, so
+    there only agreement at the 22-bit operand level is asserted; both match the oracle."""
+    old = L.precision_mode()
+    L.set_precision(lprec)
+    try:
+        H, T = 1536, 40
+        g = torch.Generator().manual_seed(1536 + T)
+        m = BL.ResLSTM(H, num_layers=2)
+        with torch.no_grad():
+            for p in m.lstm.parameters():
+                p.copy_((torch.rand(p.shape, generator=g) * 2 - 1) / np.sqrt(H))
+        x = torch.randn(64, H, T, generator=g)
+        sd = {k: v.detach() for k, v in m.state_dict().items()}
+        m.to(dev)
+        xd = x.to(dev)
+        full = m(xd).cpu()
+        y32 = m(xd[:32].contiguous()).cpu()
+        y20 = m(xd[:20].contiguous()).cpu()
+        assert L.load().bc_lstm_status(1) == 0
+    finally:
+        L._mode = old
+    if lprec == "x6":
+        assert torch.equal(y32, full[:32]), (y32 - full[:32]).abs().max()
+        assert torch.equal(y20, full[:20]), (y20 - full[:20]).abs().max()
+    else:
+        assert_close_rel(y32, full[:32], 2e-6, "h3 lstm 32 vs 64 clips")
+        assert_close_rel(y20, full[:20], 2e-6, "h3 lstm 20 vs 64 clips")
+    want = O.res_lstm(x[:20], sd, "", 2)
+    assert_close_rel(y20, want, 2e-5, f"lstm {lprec} 20 clips")
+
+
 @pytest.mark.parametrize("Cin,Cout,K,d", [(384, 384, 7, 9), (1536, 1024, 3, 1), (96, 96, 7, 1), (768, 768, 1, 1)])
 def test_x6_error_vs_fp64(dev, Cin, Cout, K, d):
     """The 3xbf16-split MFMA conv is fp32-accurate: its error against an fp64 evaluation is no larger
@@ -432,6 +468,45 @@ def test_resunit_fused_bf16(dev, C, d, causal, B, T):
     assert_close_rel(got, want, 2e-2, f"bf16 resunit C={C} d={d} vs fp32 oracle")
     rel = ((got - want).abs().max() / want.abs().max()).item()
     assert rel > 1e-5, rel  # really bf16 products
+
+
+@pytest.mark.parametrize("prec,C,alt", [("h3", 96, 309), ("bf16", 96, 209), ("x6", 96, 123), ("bf16", 48, 224),
+                                        ("bf16", 48, 206)])
+@pytest.mark.parametrize("d,B,T", [(1, 2, 1001), (9, 1, 4096), (3, 1, 129)])
+def test_resunit_tiles_bit_identical(dev, prec, C, alt, d, B, T):
+    """The one-launch ResidualUnit on another tile shape (123, the h3 / bf16 default at C = 96: 96 x 128 as 2 x 4 waves of
+    48 x 32, against 109's 8 waves of 96 x 16; 124 / 106: 48 x 512 /
+    48 x 256, 48 x 64 / 48 x 32 per wave) computes every output with the same per-output MFMA chain, the same staged
+    columns per chunk (h3 block scales) and the same h tile: bit-identical to the default tile, and within the
+    oracle's tolerance."""
+    old = L.precision_mode()
+    L.set_precision(prec)
+    try:
+        g = torch.Generator().manual_seed(C + 13 * d + T)
+        ru = BL.ResidualUnit(C, dilation=d)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            ru.block[k].act.load_state_dict(_snake(C, g).state_dict())
+        nxt = M.Activation1d(activation=_snake(C, g))
+        x = torch.randn(B, C, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        want = O.residual_unit(x, sd, "", d, False, False)
+        ru.to(dev)
+        nxt.to(dev)
+        xd = x.to(dev)
+        base = ru._fused_cfg()
+        assert base != alt
+        if prec == "h3" and C == 48:
+            pytest.skip("C = 48 h3 runs the strip kernel")
+        ref_raw, ref_act = ru._flow_fused(base, xd, None, True, nxt)
+        raw, act = ru._flow_fused(alt, xd, None, True, nxt)
+        ref_raw, ref_act, raw, act = ref_raw.cpu(), ref_act.cpu(), raw.cpu(), act.cpu()
+    finally:
+        L._mode = old
+    assert torch.equal(raw, ref_raw), f"{prec} C={C} cfg {alt} vs {base}: max |d| {(raw - ref_raw).abs().max().item():.3e}"
+    assert torch.equal(act, ref_act)
+    assert_close_rel(raw, want, 2e-2 if prec == "bf16" else 2e-5, f"{prec} resunit C={C} d={d} cfg {alt}")
 
 
 @pytest.mark.parametrize("d,B,T", [(3, 1, 1001), (3, 1, 4096), (1, 1, 24000), (9, 1, 24000), (3, 2, 700),

@@ -22,7 +22,9 @@ def main():
     p.add_argument("--model", default="default")
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--seconds", type=float, default=10.0)
+    p.add_argument("--precision", default="h3")
     a = p.parse_args()
+    L.set_precision(a.precision)
     import bench
 
     dev = torch.device("cuda", 0)
@@ -68,7 +70,7 @@ def main():
         e0.record()
         out = rorig(self, cfg, x_raw, x_act, want_raw, next_act)
         e1.record()
-        B, C, T = x_act.shape
+        B, C, T = x_raw.shape
         conv7 = BLK._conv_of(self.block[1])
         rows.append((f"resunit C={C} d={conv7.dilation} T={T}{' dual' if want_raw and next_act else ''}",
                      2.0 * B * C * C * T * 8, e0, e1))
