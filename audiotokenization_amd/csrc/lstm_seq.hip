@@ -340,10 +340,15 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
 // P = 3: x6 (3 bf16 planes, 6 products).  P = 2: h3 (2 fp16 planes, 3 products, x6_common.h): W_hh
 // rows are pre-scaled on the host by 2^(14 - e_row) (1 / scale stored after the planes), h_t in
 // (-1, 1) is split with the fixed scale 2^14, and the summed gate products are unscaled per gate row.
-template <int KS, int P>
+// NTH: 16-clip n-tiles per half.  2 (halves of 32) for launches of 33-64 clips; 1 (halves of 16) for <= 32
+// clips (BASELINE config 5 runs 32 per GPU), where halves of 32 left half 1 empty -- every step still paid its
+// poll / load / reduction / publish chain for no clips.  Same hseq layout (n-tile 1 unused), same per-cell
+// arithmetic in the same order: a clip's outputs do not depend on NTH (test_reslstm_half_split_bit_identical).
+template <int KS, int P, int NTH = 2>
 __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
   typedef typename LsFrag<P>::type frag_t;
-  constexpr int NH = 32;                       // clips per half
+  static_assert(NTH == 1 || NTH == 2, "halves of 16 or 32 clips");
+  constexpr int NH = 16 * NTH;                 // clips per half
   __shared__ floatx4 red[LS_WAVES][4][64];     // per-wave partial gates of one half's 4 tiles
   __shared__ float hs[NH][LS_U + 1];           // one half's h_t gathered per clip
   __shared__ int bail;
@@ -376,9 +381,10 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
     for (int gate = 0; gate < 4; ++gate) gsc[gate] = wsc[gate * H + g * LS_U + cu] * (1.0f / 16384.0f);
   }
   const int cbh = (w & 1) * 16 + (lane & 15);  // my cell's clip within a half
+  const bool cell = cbh < NH;                  // NTH == 1: waves 1 and 3 hold no cell
   float cst0 = 0.f, cst1 = 0.f;                // my cell's c in half 0 / half 1
   const long long unit_row = (long long)(g * LS_U + cu) * a.Btot + a.b0;  // [H][Btot] state row of my cell
-  if (a.c0) {
+  if (a.c0 && cell) {
     if (cbh < a.nb) cst0 = a.c0[unit_row + cbh];
     if (NH + cbh < a.nb) cst1 = a.c0[unit_row + NH + cbh];
   }
@@ -418,7 +424,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
       const int clip = h * NH + cbh;
-      hs[cbh][cu] = clip < a.nb ? a.h0[unit_row + clip] : 0.f;
+      if (cell) hs[cbh][cu] = clip < a.nb ? a.h0[unit_row + clip] : 0.f;
       __syncthreads();
       publish_slot(0, h);
       __syncthreads();
@@ -446,7 +452,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
   if (stamp_row && ts < LS_STAMP_T) stamp_row[(ts * 4 + w) * 8 + (ev)] = (long long)__builtin_amdgcn_s_memtime();
       LS2_STAMP(0)
       const int clip = h * NH + cbh;
-      const bool ok = clip < a.nb;
+      const bool ok = cell && clip < a.nb;
       float gxv[4];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate)
@@ -489,7 +495,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         auto load_ks = [&](int ks, frag_t (&dst)[2][P]) {
           const int ksa = w * KS + ks;
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
+          for (int nt = 0; nt < NTH; ++nt)
 #pragma unroll
             for (int p = 0; p < P; ++p)
               dst[nt][p] = ls_load_sc1<frag_t>(hr, (unsigned)((((ksa * 2 + nt) * P + p) * 64 + lane) * 16));
@@ -501,7 +507,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
           if (ks + HD - 1 < KS) load_ks(ks + HD - 1, hbuf[(ks + HD - 1) % HD]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
+          for (int nt = 0; nt < NTH; ++nt) {
             const frag_t* hb = hbuf[ks % HD][nt];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -560,7 +566,7 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
       if (h) cst1 = c;
       else cst0 = c;
       const float hq = ok ? og * ls_tanh(c) : 0.f;
-      hs[cbh][cu] = hq;
+      if (cell) hs[cbh][cu] = hq;
       LS2_STAMP(4)
       __syncthreads();
       LS2_STAMP(5)
@@ -722,8 +728,9 @@ static bool all_resident(K kernel, int G) {
 static bool seq_resident(int KS, int planes, bool halves, int G) {
 #define BC_LS_RES(K)                                                                        \
   case K:                                                                                   \
-    if (planes == 2) return all_resident(lstm_seq2_x6_kernel<K, 2>, G);                     \
-    if (halves) return all_resident(lstm_seq2_x6_kernel<K, 3>, G);                          \
+    if (planes == 2)                                                                        \
+      return all_resident(lstm_seq2_x6_kernel<K, 2>, G) && all_resident(lstm_seq2_x6_kernel<K, 2, 1>, G); \
+    if (halves) return all_resident(lstm_seq2_x6_kernel<K, 3>, G) && all_resident(lstm_seq2_x6_kernel<K, 3, 1>, G); \
     return all_resident(lstm_seq_x6_kernel<K>, G);
   switch (KS) {
     BC_LS_RES(2)
@@ -777,14 +784,24 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
   int& rs = resident_checked[ks_idx][planes == 2 ? 0 : 1];
   if (rs == 0) rs = seq_resident(H / 128, planes, halves, G) ? 1 : -1;
   if (rs < 0) return BC_ERR_UNSUPPORTED;
+  // BC_LSTM_NH16=0 keeps launches of <= 32 clips on halves of 32 (A/B timing)
+  static const bool nh16 = [] {
+    const char* e = getenv("BC_LSTM_NH16");
+    return !(e && atoi(e) == 0);
+  }();
   for (int b0 = 0; b0 < Btot; b0 += LS_NB) {
     a.b0 = b0;
     a.nb = Btot - b0 < LS_NB ? Btot - b0 : LS_NB;
+    const bool h16 = nh16 && a.nb <= 32;
     if (hipMemsetAsync(a.flags, 0, LS_FLAG_BYTES, st) != hipSuccess) return BC_ERR_LAUNCH;
 #define BC_LS_CASE(KS)                                                                      \
   case KS:                                                                                  \
-    if (planes == 2)                                                                        \
+    if (planes == 2 && h16)                                                                 \
+      hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 2, 1>), dim3(G), dim3(256), 0, st, a);    \
+    else if (planes == 2)                                                                   \
       hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 2>), dim3(G), dim3(256), 0, st, a);       \
+    else if (halves && h16)                                                                 \
+      hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 3, 1>), dim3(G), dim3(256), 0, st, a);    \
     else if (halves)                                                                        \
       hipLaunchKernelGGL((lstm_seq2_x6_kernel<KS, 3>), dim3(G), dim3(256), 0, st, a);       \
     else                                                                                    \
