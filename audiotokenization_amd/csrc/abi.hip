@@ -209,16 +209,27 @@ int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode)
 }
 
 // workspace: status [64 floats: int32 timeout count of this call] | xt [H][T*B] | gx [4H][T*B] |
-// y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2
+// y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2 or the persistent kernel's region | the input projection's
+// pre-split B planes (pw_presplit.hip, h3)
 constexpr long long LSTM_WS_STATUS_FLOATS = 64;
 static long long lstm_frag_floats(int B, int H) { return (long long)((B + 63) / 64) * 64 * H; }
+static long long lstm_ws_head_floats(int B, int H, int T) {
+  const long long tb = (long long)T * B;
+  const long long frag = 2 * lstm_frag_floats(B, H);
+  const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
+  return (LSTM_WS_STATUS_FLOATS + tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq) + 3) / 4 * 4;
+}
+// The input projection on the pre-split GEMM (h3, Cout % 192 == 0, Cin % 32 == 0): on by default; BC_LSTM_PRESPLIT=0
+// or bc_debug_set_lstm_presplit(0) runs it on conv1d_x6_kernel (A/B timing, the bit-identity test).
+static int g_lstm_presplit = [] {
+  const char* e = getenv("BC_LSTM_PRESPLIT");
+  return e && atoi(e) == 0 ? 0 : 1;
+}();
 
 long long bc_lstm_workspace_floats(int B, int H, int T) {
   if (B < 0 || H <= 0 || T < 0) return -1;
   const long long tb = (long long)T * B;
-  const long long frag = 2 * lstm_frag_floats(B, H);
-  const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
-  return LSTM_WS_STATUS_FLOATS + tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq);
+  return lstm_ws_head_floats(B, H, T) + (pw_presplit_bytes(H, tb > 0 ? tb : 1) + 3) / 4;
 }
 
 static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num_layers,
@@ -249,7 +260,8 @@ int bc_reslstm_fwd_state(const float* x, float* out, int B, int H, int T, int nu
 // channels), then the recurrence into lout [H][T*B] (the persistent kernel, or one launch per step).
 static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const float* bias, const float* whh,
                           float* lout, float* gx, float* cst, float* const (&frag)[2], int B, int H, int T, int mode,
-                          hipStream_t st, const float* h0, const float* c0, float* hT, float* cT, int* call_status) {
+                          hipStream_t st, const float* h0, const float* c0, float* hT, float* cT, int* call_status,
+                          void* psplit = nullptr) {
   const long long tb = (long long)T * B;
   if (!wih || !whh || !bias) return BC_ERR_ARG;
   ConvArgs a{};
@@ -259,7 +271,12 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   a.Cin = Cin; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
   a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
   a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
-  int rc = conv_launch(a, 1, conv_select_cfg(4 * H, Cin, 1, 1, 1, mode), st);
+  const int cfg = conv_select_cfg(4 * H, Cin, 1, 1, 1, mode);
+  int rc;
+  if (psplit && g_lstm_presplit && cfg == 322 && pw_presplit_ok(4 * H, Cin, tb))
+    rc = pw_presplit_launch(a, psplit, st);  // same planes, scales and MFMA chains as cfg 322: bit-identical
+  else
+    rc = conv_launch(a, 1, cfg, st);
   if (rc) return rc;
   if (lstm_use_seq(H, mode))  // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
     return lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(whh), lout, cst, H, T, B, lstm_planes(mode), st,
@@ -304,7 +321,7 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
     const long long so = (long long)l * H * B;  // layer l's [H][B] state
     rc = lstm_layer_dir(lin, H, w_ih_packed[l], bias[l], w_hh_packed[l], lout, gx, cst, frag, B, H, T, mode, st,
                         h0 ? h0 + so : nullptr, c0 ? c0 + so : nullptr, hT ? hT + so : nullptr,
-                        cT ? cT + so : nullptr, call_status);
+                        cT ? cT + so : nullptr, call_status, workspace + lstm_ws_head_floats(B, H, T));
     if (rc) return rc;
     lin = lout;
     lout = (lout == ya) ? yb : ya;
@@ -460,3 +477,11 @@ int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream) 
 }
 
 }  // extern "C"
+
+// Diagnostics only (not part of include/bigcodec.h): run the unidirectional ResLSTM's input projection on the
+// pre-split GEMM (1, the default) or on conv1d_x6_kernel (0); returns the previous setting.
+extern "C" int bc_debug_set_lstm_presplit(int on) {
+  const int old = g_lstm_presplit;
+  g_lstm_presplit = on ? 1 : 0;
+  return old;
+}

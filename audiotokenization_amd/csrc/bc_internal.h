@@ -49,6 +49,10 @@ int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
 
 int resunit_select_cfg(int C, int d, int mode);
 bool resunit_cfg_ok(int cfg, int C, int d);
+// pointwise GEMM with a pre-split B operand (pw_presplit.hip; the ResLSTM input projection in h3)
+long long pw_presplit_bytes(int Cin, long long N);
+bool pw_presplit_ok(int Cout, int Cin, long long N);
+int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,

@@ -1,0 +1,248 @@
+// Pointwise GEMM with a pre-split B operand: the ResLSTM input projection gx = W_ih x + b over T*B columns
+// (vq/module.py:143-167 -> nn.LSTM's input-hidden product; Cin = H = 1536, Cout = 4H = 6144 in the default
+// model), h3 operands.
+//
+// On the 16-wave 192 x 256 tile (cfg 322) every m-tile workgroup re-stages the same B chunk: 32 of them per
+// column tile here, each loading 32 channels x 256 columns of fp32, taking the block maximum, splitting into two
+// fp16 planes and storing them to LDS, between two barriers and with no MFMA to overlap (one chunk = one K-step
+// for a pointwise conv).  Measured: 6.7k cycles per chunk-step against 2.3k of MFMA.  Here:
+//   presplit_b_kernel  one pass over x: per 256-column tile and 32-channel chunk the block scale exactly as the
+//                      GEMM's staging computes it (h3_scale_from_bits of the block maximum, out-of-range columns
+//                      zero; the running minimum over the tile's chunks so far), and the two fp16 planes of
+//                      x * scale in the GEMM's LDS image ([col][64 B], 16-B channel groups XOR-swizzled by
+//                      (col >> 1) & 3), so the GEMM copies them with LDS-DMA like the weights;
+//   pw_presplit_kernel the 16-wave tile's main loop with B by LDS-DMA (double-buffered A and B, one barrier per
+//                      chunk, no staging VALU), the same MFMA chain per output and the same exact power-of-two
+//                      accumulator rescale when the scale decreases, the shared h3 epilogue.
+// Same blocks, same scales, same products in the same order: bit-identical to conv1d_x6_kernel on cfg 322
+// (tests/test_gpu_kernels.py::test_lstm_projection_presplit_bit_identical).
+#include "bc_common.h"
+#include "bc_internal.h"
+#include "conv_epilogue.h"
+#include "x6_common.h"
+
+namespace bc {
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int PS_BN = 256;             // columns per tile: the 16-wave tile's BN (the same staged blocks)
+constexpr int PS_PLANE = PS_BN * 64;   // bytes of one fp16 plane of a chunk (32 channels per column)
+constexpr int PS_MT = 6, PS_NT = 2, PS_WM = 2, PS_WN = 8;
+constexpr int PS_QA = PS_WM * PS_MT;   // 12 m-tiles of 16 rows
+constexpr int PS_APIECES = 2 * PS_QA;  // 1-KiB pieces of a chunk's A block (2 planes)
+constexpr int PS_BPIECES = 2 * PS_PLANE / 1024;  // 32 pieces of a chunk's B block
+constexpr int PS_BBUF = 3;             // B buffers: chunk c + 2's planes are in flight while chunk c computes
+constexpr int PS_LDS = PS_BBUF * 2 * PS_PLANE + 2 * PS_APIECES * 1024;  // 144 KiB
+
+// One 256-thread workgroup per 256-column tile: wave w holds channels 8w .. 8w + 7 of each chunk, lane l the
+// columns 4l .. 4l + 3 (16-byte loads, 1 KiB per channel row per wave).
+__global__ void __launch_bounds__(256) presplit_b_kernel(const float* __restrict__ x, unsigned char* __restrict__ planes,
+                                                         float* __restrict__ scales, int Cin, int N, int nch) {
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = j * PS_BN + 4 * lane;
+  __shared__ unsigned wmax[4];
+  float xs = 1.f;
+  for (int c = 0; c < nch; ++c) {
+    float v[8][4];
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ch = c * X6_BKC + 8 * w + k;
+      const float* row = x + (long long)ch * N;
+      if (ch < Cin && n + 3 < N && (N & 3) == 0) {  // 16-byte aligned rows
+        const floatx4 q = *reinterpret_cast<const floatx4*>(row + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[k][r] = q[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[k][r] = (ch < Cin && n + r < N) ? row[n + r] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const unsigned u = __float_as_uint(fabsf(v[k][r]));
+        m = m > u ? m : u;
+      }
+    }
+    m = wave_max_u32(m);
+    if (lane == 0) wmax[w] = m;
+    __syncthreads();
+    unsigned mm = wmax[0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) mm = mm > wmax[q] ? mm : wmax[q];
+    const float s = h3_scale_from_bits(__builtin_amdgcn_readfirstlane(mm));
+    xs = c == 0 ? s : (s < xs ? s : xs);  // the GEMM's staging: chunk 0's scale, then the running minimum
+    __syncthreads();                      // wmax is rewritten by the next chunk
+    if (tid == 0) scales[(long long)j * nch + c] = xs;
+    unsigned char* pb = planes + ((long long)j * nch + c) * (2 * PS_PLANE);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = 4 * lane + r;
+      unsigned h[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) split2_h(v[2 * k][r] * xs, v[2 * k + 1][r] * xs, h[k], l[k]);
+      const int off = col * 64 + 16 * (w ^ ((col >> 1) & 3));
+      *reinterpret_cast<u32x4_t*>(pb + off) = (u32x4_t){h[0], h[1], h[2], h[3]};
+      *reinterpret_cast<u32x4_t*>(pb + PS_PLANE + off) = (u32x4_t){l[0], l[1], l[2], l[3]};
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024, 1) pw_presplit_kernel(ConvArgs a, const unsigned char* __restrict__ planes,
+                                                              const float* __restrict__ scales) {
+  constexpr int MT = PS_MT, NT = PS_NT, WM = PS_WM, NW = PS_WM * PS_WN;
+  typedef f16x8_t frag_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_ps[];
+  unsigned char* Bs = smem_ps;                           // [3][2 planes][PS_PLANE]
+  unsigned char* As = smem_ps + PS_BBUF * 2 * PS_PLANE;  // [2][2 planes][QA][1 KiB]
+
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int mt_idx = wg % a.ntm;
+  const int nt_idx = wg / a.ntm;
+  const int m0 = mt_idx * 16 * MT * WM;
+  const int n0 = nt_idx * PS_BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int nch = a.nchunks;
+
+  const unsigned char* wblk = reinterpret_cast<const unsigned char*>(a.w) + (long long)mt_idx * nch * (PS_APIECES * 1024);
+  const unsigned char* bblk = planes + (long long)nt_idx * nch * (2 * PS_PLANE);
+  const float* sblk = scales + (long long)nt_idx * nch;
+  // chunk c's A block (24 pieces; A buffer c & 1) and B block (32 pieces, exactly 2 per wave; B buffer c % 3),
+  // spread over the 16 waves
+  static_assert(PS_BPIECES == 2 * NW, "two B pieces per wave (the counted wait below)");
+  auto issue_a = [&](int c) {
+    const unsigned char* sa = wblk + (long long)c * (PS_APIECES * 1024);
+    unsigned char* da = As + (c & 1) * (PS_APIECES * 1024);
+    for (int q = wave; q < PS_APIECES; q += NW)
+      __builtin_amdgcn_global_load_lds((const void*)(sa + q * 1024 + lane * 16), (lds_void_t)(da + q * 1024), 16, 0, 0);
+  };
+  auto issue_b = [&](int c) {
+    const unsigned char* sb = bblk + (long long)c * (2 * PS_PLANE);
+    unsigned char* db = Bs + (c % PS_BBUF) * (2 * PS_PLANE);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = wave + k * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(sb + q * 1024 + lane * 16), (lds_void_t)(db + q * 1024), 16, 0, 0);
+    }
+  };
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int col_lane = wn * NT * 16 + (lane & 15);
+  const int bgo = col_lane * 64 + 16 * ((lane >> 4) ^ ((col_lane >> 1) & 3));  // conv1d_x6_kernel's bgrp
+  // one chunk: this wave's MT x NT tiles, A fragments one m-tile ahead (conv1d_x6_kernel's compute, h3)
+  auto compute = [&](int c) {
+    const unsigned char* Ab = As + (c & 1) * (PS_APIECES * 1024);
+    const unsigned char* Bcol = Bs + (c % PS_BBUF) * (2 * PS_PLANE) + bgo;
+    frag_t bf[NT][2];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * 64 + p * PS_PLANE);
+    frag_t af[2][2];
+    auto load_a = [&](int i, frag_t (&d)[2]) {
+      const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) d[p] = *reinterpret_cast<const frag_t*>(Aq + p * PS_QA * 1024);
+    };
+    load_a(0, af[0]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      const frag_t a0 = af[i & 1][0], a1 = af[i & 1][1];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        if (j == 1 && i + 1 < MT) {
+          __builtin_amdgcn_sched_barrier(0);
+          load_a(i + 1, af[(i + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        floatx4 t = acc[i][j];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][1], a0, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a1, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][0], a0, t, 0, 0, 0);
+        acc[i][j] = t;
+      }
+    }
+  };
+
+  // issue order per wave: B(0), A(0), B(1) | step c: A(c + 1), B(c + 2), compute, counted wait, barrier.  vmcnt
+  // retires in issue order, so at the end of step c a wait for all but this wave's 2 youngest pieces (B(c + 2))
+  // retires A(c + 1) and B(c + 1); the barrier then publishes every wave's pieces and frees A buffer c & 1 and B
+  // buffer c % 3 (rewritten by A(c + 2) / B(c + 3), issued in steps c + 1 / c + 1).
+  issue_b(0);
+  issue_a(0);
+  dma_issue_order();
+  if (nch > 1) issue_b(1);
+  float xs = sblk[0];
+  if (nch > 1) wait_vmcnt<2>();
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) issue_a(c + 1);
+    dma_issue_order();
+    if (c + 2 < nch) issue_b(c + 2);
+    dma_issue_order();
+    compute(c);
+    if (c + 1 < nch) {  // chunk c + 1 was split at the running-minimum scale: follow it exactly (powers of two)
+      const float sn = sblk[c + 1];
+      if (sn < xs) {
+        const float r = sn / xs;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] *= r;
+        xs = sn;
+      }
+    }
+    if (c + 2 < nch)
+      wait_vmcnt<2>();  // this wave's pieces of A(c + 1) and B(c + 1) have landed; B(c + 2) may stay in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  }
+  conv_epilogue<MT, NT, true>(a, acc, 0, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
+}
+
+long long pw_presplit_bytes(int Cin, long long N) {
+  const long long ntn = (N + PS_BN - 1) / PS_BN, nch = (Cin + X6_BKC - 1) / X6_BKC;
+  return ntn * nch * (2LL * PS_PLANE + 4);
+}
+
+bool pw_presplit_ok(int Cout, int Cin, long long N) {
+  return Cout % (16 * PS_MT * PS_WM) == 0 && Cin % X6_BKC == 0 && N > 0 && N <= 0x7fffffffLL &&
+         (long long)Cin * N * 4 <= 0x7fffffffffffLL;
+}
+
+// a: the pointwise conv as conv_launch would run it on cfg 322 (K = 1, stride 1, one batch item, x [Cin][N],
+// y [Cout][N]); w packed for cfg 322.  ws: pw_presplit_bytes(Cin, N) bytes (planes, then the scales).
+int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st) {
+  if (a.K != 1 || a.s != 1 || a.d != 1 || a.pl != 0 || a.ps || !ws) return BC_ERR_ARG;
+  if (!pw_presplit_ok(a.Cout, a.Cin, a.Nout) || a.Tin != a.Nout) return BC_ERR_UNSUPPORTED;
+  const long long N = a.Nout;
+  const int ntn = (int)((N + PS_BN - 1) / PS_BN), nch = a.Cin / X6_BKC;
+  unsigned char* planes = reinterpret_cast<unsigned char*>(ws);
+  float* scales = reinterpret_cast<float*>(planes + (long long)ntn * nch * 2 * PS_PLANE);
+  hipLaunchKernelGGL(presplit_b_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, scales, a.Cin, (int)N, nch);
+  BC_CHECK_LAUNCH();
+  a.vec = conv_epilogue_vec_ok(a);
+  a.ntm = a.Cout / (16 * PS_MT * PS_WM);
+  a.ntn = ntn;
+  a.nchunks = nch;
+  const long long nwg = (long long)a.ntm * ntn;
+  if (nwg > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  a.nwg = (int)nwg;
+  a.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
+                                         (long long)a.ntm * nch * PS_APIECES * 1024);  // 1 / row scales after the planes
+  hipLaunchKernelGGL(pw_presplit_kernel, dim3(a.nwg), dim3(1024), PS_LDS, st, a, planes, scales);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+}  // namespace bc

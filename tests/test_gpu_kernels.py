@@ -288,6 +288,38 @@ def test_reslstm(dev, H, layers, B, T, prec):
     assert L.load().bc_lstm_status(1) == 0
 
 
+@pytest.mark.parametrize("H,B,T", [(1536, 3, 100), (768, 2, 700), (1536, 64, 40)])
+def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
+    """h3: the ResLSTM input projection on the pre-split GEMM (pw_presplit.hip: B planes and block scales made once
+    per 256-column tile, copied by LDS-DMA) against the same projection on conv1d_x6_kernel cfg 322: the same
+    blocks, scales and MFMA chains, so the layer outputs are bit-identical; T * B not a multiple of 256 (ragged last
+    column tile) included; and within the oracle's tolerance."""
+    old = L.precision_mode()
+    L.set_precision("h3")
+    lib = L.load()
+    try:
+        g = torch.Generator().manual_seed(H * 3 + B + T)
+        m = BL.ResLSTM(H, num_layers=2)
+        with torch.no_grad():
+            for p in m.lstm.parameters():
+                p.copy_((torch.rand(p.shape, generator=g) * 2 - 1) / np.sqrt(H))
+        x = torch.randn(B, H, T, generator=g) * torch.exp(torch.randn(1, H, 1, generator=g))
+        sd = {k: v.detach() for k, v in m.state_dict().items()}
+        m.to(dev)
+        xd = x.to(dev)
+        prev = lib.bc_debug_set_lstm_presplit(1)
+        y_ps = m(xd).cpu()
+        lib.bc_debug_set_lstm_presplit(0)
+        y_x6 = m(xd).cpu()
+        lib.bc_debug_set_lstm_presplit(prev)
+        assert lib.bc_lstm_status(1) == 0
+    finally:
+        L._mode = old
+    assert torch.equal(y_ps, y_x6), (y_ps - y_x6).abs().max()
+    want = O.res_lstm(x, sd, "", 2)
+    assert_close_rel(y_ps, want, 2e-5, f"lstm h3 presplit H={H}")
+
+
 @pytest.mark.parametrize("lprec", ["h3", "x6"])
 def test_reslstm_half_split_bit_identical(dev, lprec):
     """The persistent recurrence runs a launch of <= 32 clips as two halves of 16 (NTH = 1) and a launch of 33-64
