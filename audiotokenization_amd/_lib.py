@@ -32,6 +32,8 @@ _SIGS = {
     "bc_resunit_fwd_snake_in": (I, [P] * 13 + [I] * 6 + [P]),
     "bc_convT1d_phase_taps": (I, [I, I]),
     "bc_convT1d_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P]),
+    "bc_convT1d_workspace_floats": (L, [I, I, I, I, I, I, I]),
+    "bc_convT1d_fwd_ws": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P, P]),
     "bc_snake_fwd": (I, [P, P, P, P, I, I, L, P]),
     "bc_aa_snake_fwd": (I, [P, P, P, P, P, P, I, I, I, P]),
     "bc_aa_snake_out_len": (L, [I, I, I, I]),
@@ -63,7 +65,7 @@ _SIGS = {
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 10  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 11  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

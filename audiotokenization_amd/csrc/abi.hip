@@ -107,6 +107,72 @@ int bc_convT1d_phase_taps(int K, int stride) {
   return (K + stride - 1) / stride;
 }
 
+// phase r of a transposed conv: outputs t = s*q - p + r for q in [q_lo, q_lo + nout)
+static void convT_phase(int r, int s, int p, int Tout, int* q_lo, int* nout) {
+  const int lo = (p - r + s - 1 >= 0) ? (p - r + s - 1) / s : -((r - p) / s);
+  const long long q_hi_num = (long long)Tout - 1 + p - r;
+  const int hi = q_hi_num >= 0 ? (int)(q_hi_num / s) : -1;
+  *q_lo = lo;
+  *nout = hi - lo + 1;
+}
+// contiguous per-phase rows of the workspace: Q4 = max phase length rounded up to 4 (16-byte epilogue rows)
+static int convT_q4(int Tout, int s, int p) {
+  int qmax = 0;
+  for (int r = 0; r < s; ++r) {
+    int lo, n;
+    convT_phase(r, s, p, Tout, &lo, &n);
+    qmax = n > qmax ? n : qmax;
+  }
+  return (qmax + 3) / 4 * 4;
+}
+
+long long bc_convT1d_workspace_floats(int B, int Cout, int Tout, int K, int stride, int padding, int dual) {
+  if (B < 0 || Cout <= 0 || Tout < 0 || K <= 0 || stride <= 0 || stride > CONVT_MAX_STRIDE || padding < 0) return -1;
+  return (long long)stride * B * Cout * convT_q4(Tout, stride, padding) * (dual ? 2 : 1);
+}
+
+int bc_convT1d_fwd_ws(const float* x, const float* const* w_phases, const float* bias,
+                      const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
+                      float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+                      int padding, int cfg, float* workspace, void* stream) {
+  if (!workspace)
+    return bc_convT1d_fwd(x, w_phases, bias, out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, Cin, Tin, Cout, Tout, K,
+                          stride, padding, cfg, stream);
+  if (!x || !w_phases || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 || stride <= 0 ||
+      stride > CONVT_MAX_STRIDE || padding < 0 || !conv_cfg_valid(cfg))
+    return BC_ERR_ARG;
+  if ((out_snake_alpha_exp == nullptr) != (out_snake_inv_beta == nullptr)) return BC_ERR_ARG;
+  if (y2 && !out_snake_alpha_exp) return BC_ERR_ARG;
+  const int s = stride, p = padding;
+  const int Kp = (K + s - 1) / s;
+  if (!cfg_matches(cfg, Cout, Cin, Kp, 1, 1)) return BC_ERR_ARG;
+  if (B == 0 || Tout == 0) return BC_OK;
+  const int Q4 = convT_q4(Tout, s, p);
+  const long long plane = (long long)B * Cout * Q4;  // one phase's rows
+  float* w2 = y2 ? workspace + s * plane : nullptr;
+  ConvTInterleave il{};
+  il.s = s;
+  il.p = p;
+  for (int r = 0; r < s; ++r) {
+    if (!w_phases[r]) return BC_ERR_ARG;
+    int q_lo, nout;
+    convT_phase(r, s, p, Tout, &q_lo, &nout);
+    il.q_lo[r] = q_lo;
+    if (nout <= 0) continue;
+    ConvArgs a{};
+    a.x = x; a.w = w_phases[r]; a.bias = bias; a.res = nullptr;
+    a.osa = out_snake_alpha_exp; a.osb = out_snake_inv_beta; a.y = workspace + r * plane; a.y2 = w2 ? w2 + r * plane : nullptr;
+    a.xbs = (long long)Cin * Tin; a.ybs = (long long)Cout * Q4; a.rbs = 0;
+    a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = nout;
+    a.K = Kp; a.s = 1; a.d = 1; a.pl = Kp - 1 - q_lo;  // as bc_convT1d_fwd
+    a.yT = Q4; a.ostride = 1; a.ooff = 0; a.epi = 0;
+    if (a.pl < 0) return BC_ERR_UNSUPPORTED;
+    const int rc = conv_launch(a, B, cfg, S(stream));
+    if (rc != BC_OK) return rc;
+  }
+  return convT_interleave_launch(workspace, w2, y, y2, B, Cout, Tout, Q4, il, S(stream));
+}
+
 int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bias,
                    const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
                    float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,

@@ -49,6 +49,14 @@ int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st);
 
 int resunit_select_cfg(int C, int d, int mode);
 bool resunit_cfg_ok(int cfg, int C, int d);
+// ConvTranspose1d: the phase rows of bc_convT1d_fwd_ws's workspace -> the output in order (elementwise.hip)
+constexpr int CONVT_MAX_STRIDE = 16;
+struct ConvTInterleave {
+  int s, p;
+  int q_lo[CONVT_MAX_STRIDE];
+};
+int convT_interleave_launch(const float* ph, const float* ph2, float* y, float* y2, int B, int Cout, int Tout, int Q4,
+                            const ConvTInterleave& il, hipStream_t st);
 // pointwise GEMM with a pre-split B operand (pw_presplit.hip; the ResLSTM input projection in h3)
 long long pw_presplit_bytes(int Cin, long long N);
 bool pw_presplit_ok(int Cout, int Cin, long long N);

@@ -351,4 +351,53 @@ int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_
   return BC_OK;
 }
 
+// ConvTranspose1d interleave (bc_convT1d_fwd_ws): output t of row (b, co) is phase r = (t + p) mod s, position
+// q = (t + p) div s of that phase, i.e. element q - q_lo[r] of the phase's contiguous row (b, co) in the workspace.
+// One thread per 4 consecutive outputs (16-byte stores where the row allows).
+__global__ void __launch_bounds__(256) convT_interleave_kernel(const float* __restrict__ ph, const float* __restrict__ ph2,
+                                                               float* __restrict__ y, float* __restrict__ y2, int Tout,
+                                                               int Q4, long long plane, ConvTInterleave il) {
+  const long long row = blockIdx.y;  // b * Cout + co
+  const int t0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (t0 >= Tout) return;
+  float v[4], v2[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int t = t0 + k;
+    if (t >= Tout) break;
+    const int u = t + il.p;
+    const int r = u % il.s, q = u / il.s;
+    const long long src = r * plane + row * Q4 + (q - il.q_lo[r]);
+    v[k] = ph[src];
+    if (ph2) v2[k] = ph2[src];
+  }
+  float* yr = y + row * Tout;
+  float* y2r = y2 ? y2 + row * Tout : nullptr;
+  if (t0 + 3 < Tout && (Tout & 3) == 0) {
+    *reinterpret_cast<floatx4*>(yr + t0) = floatx4{v[0], v[1], v[2], v[3]};
+    if (y2r) *reinterpret_cast<floatx4*>(y2r + t0) = floatx4{v2[0], v2[1], v2[2], v2[3]};
+  } else {
+    for (int k = 0; k < 4 && t0 + k < Tout; ++k) {
+      yr[t0 + k] = v[k];
+      if (y2r) y2r[t0 + k] = v2[k];
+    }
+  }
+}
+
+int convT_interleave_launch(const float* ph, const float* ph2, float* y, float* y2, int B, int Cout, int Tout, int Q4,
+                            const ConvTInterleave& il, hipStream_t st) {
+  const long long rows = (long long)B * Cout;
+  if (rows <= 0 || Tout <= 0) return BC_OK;
+  if (rows > 65535 * 1024LL) return BC_ERR_UNSUPPORTED;
+  const int gx = (Tout + 1023) / 1024;
+  // grid.y is limited to 65535: fold the rows into chunks
+  for (long long r0 = 0; r0 < rows; r0 += 65535) {
+    const int ny = (int)(rows - r0 < 65535 ? rows - r0 : 65535);
+    hipLaunchKernelGGL(convT_interleave_kernel, dim3(gx, ny), dim3(256), 0, st, ph + r0 * Q4, ph2 ? ph2 + r0 * Q4 : nullptr,
+                       y + r0 * Tout, y2 ? y2 + r0 * Tout : nullptr, Tout, Q4, (long long)rows * Q4, il);
+    BC_CHECK_LAUNCH();
+  }
+  return BC_OK;
+}
+
 }  // namespace bc

@@ -111,11 +111,17 @@ std::vector<Tensor> conv_transpose1d(const Tensor& x, at::TensorList w_phases, c
   const int64_t B = x.size(0);
   auto y = at::empty({B, cout, tout}, x.options());
   Tensor y2 = dual ? at::empty_like(y) : Tensor();
-  ok(bc_convT1d_fwd(x.data_ptr<float>(), ph.data(), optf(x, bias, "bias"), optf(x, sa, "snake_alpha_exp"),
-                    optf(x, sb, "snake_inv_beta"), y.data_ptr<float>(), dual ? y2.data_ptr<float>() : nullptr,
-                    i32(B, "B"), i32(x.size(1), "Cin"), i32(x.size(2), "T"), i32(cout, "Cout"), i32(tout, "Tout"),
-                    i32(k, "K"), i32(stride, "stride"), i32(padding, "padding"), i32(cfg, "cfg"), stream_of(x)),
-     "bc_convT1d_fwd");
+  // per-phase contiguous rows + one interleave pass (bc_convT1d_fwd_ws): the same values as the strided-store path
+  const long long nws = bc_convT1d_workspace_floats(i32(B, "B"), i32(cout, "Cout"), i32(tout, "Tout"), i32(k, "K"),
+                                                    i32(stride, "stride"), i32(padding, "padding"), dual ? 1 : 0);
+  TORCH_CHECK_VALUE(nws >= 0, "bigcodec::conv_transpose1d: bad shape for the workspace query");
+  auto ws = at::empty({(int64_t)(nws > 0 ? nws : 1)}, x.options());
+  ok(bc_convT1d_fwd_ws(x.data_ptr<float>(), ph.data(), optf(x, bias, "bias"), optf(x, sa, "snake_alpha_exp"),
+                       optf(x, sb, "snake_inv_beta"), y.data_ptr<float>(), dual ? y2.data_ptr<float>() : nullptr,
+                       i32(B, "B"), i32(x.size(1), "Cin"), i32(x.size(2), "T"), i32(cout, "Cout"), i32(tout, "Tout"),
+                       i32(k, "K"), i32(stride, "stride"), i32(padding, "padding"), i32(cfg, "cfg"), ws.data_ptr<float>(),
+                       stream_of(x)),
+     "bc_convT1d_fwd_ws");
   if (dual) return {y, y2};
   return {y};
 }

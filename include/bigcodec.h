@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 10
+#define BC_ABI_VERSION 11
 
 int bc_abi_version(void);
 
@@ -105,6 +105,18 @@ int bc_convT1d_fwd(const float* x, const float* const* w_phases, const float* bi
                    const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
                    float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
                    int padding, int cfg, void* stream);
+/* bc_convT1d_fwd_ws (ABI 11): the same transposed convolution and the same values bit for bit, with a
+ * workspace of bc_convT1d_workspace_floats(B, Cout, Tout, K, stride, padding, dual) device floats
+ * (dual = y2 != NULL): each phase writes its outputs contiguously (16-byte stores) into the workspace
+ * and one interleave pass writes y (and y2) in order.  bc_convT1d_fwd writes every phase straight into
+ * y with stride-`stride` scalar stores (each output line written in `stride` partial passes); the
+ * decoder's stride-5 upsampler ran 2x slower that way.  workspace NULL: as
+ * bc_convT1d_fwd. */
+long long bc_convT1d_workspace_floats(int B, int Cout, int Tout, int K, int stride, int padding, int dual);
+int bc_convT1d_fwd_ws(const float* x, const float* const* w_phases, const float* bias,
+                      const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
+                      float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
+                      int padding, int cfg, float* workspace, void* stream);
 
 /* ---- SnakeBeta / anti-aliased Activation1d -------------------------------------------------------
  * bc_snake_fwd replaces SnakeBeta.forward (vq/activations.py:107-118).

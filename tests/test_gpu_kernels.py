@@ -205,6 +205,16 @@ def test_conv_transpose1d(dev, case, prec):
     torch.cuda.synchronize()
     assert got.shape == want.shape
     assert_close_rel(got.cpu(), want, 1e-5, f"convT {case}")
+    # the op runs bc_convT1d_fwd_ws (contiguous phase rows + interleave); the strided-store bc_convT1d_fwd computes
+    # the same phases with the same kernels: bit-identical
+    inner = m.conv if hasattr(m, "conv") and isinstance(m.conv, CV.ConvTranspose1dWN) else m
+    _, wptrs, bias, cfg = inner.prepared(dev)
+    xd = x.to(dev)
+    ref = torch.empty_like(got)
+    L.call("bc_convT1d_fwd", xd.data_ptr(), wptrs, L.ptr(bias), 0, 0, ref.data_ptr(), 0, B, Cin, T, Cout,
+           got.shape[-1], inner.kernel_size, inner.stride, inner.padding, cfg, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got), (ref - got).abs().max()
     if use_snake:
         co = snake.to(dev).coeffs(dev)
         raw, act = m.run(x.to(dev), out_snake=co, dual=True)
@@ -288,12 +298,12 @@ def test_reslstm(dev, H, layers, B, T, prec):
     assert L.load().bc_lstm_status(1) == 0
 
 
-@pytest.mark.parametrize("H,B,T", [(1536, 3, 100), (768, 2, 700), (1536, 64, 40)])
+@pytest.mark.parametrize("H,B,T", [(1536, 3, 100), (768, 2, 700), (1536, 64, 40), (768, 3, 33)])
 def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
     """h3: the ResLSTM input projection on the pre-split GEMM (pw_presplit.hip: B planes and block scales made once
     per 256-column tile, copied by LDS-DMA) against the same projection on conv1d_x6_kernel cfg 322: the same
     blocks, scales and MFMA chains, so the layer outputs are bit-identical; T * B not a multiple of 256 (ragged last
-    column tile) included; and within the oracle's tolerance."""
+    column tile) and not a multiple of 4 (no 16-byte rows) included; and within the oracle's tolerance."""
     old = L.precision_mode()
     L.set_precision("h3")
     lib = L.load()

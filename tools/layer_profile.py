@@ -23,6 +23,7 @@ def main():
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--seconds", type=float, default=10.0)
     p.add_argument("--precision", default="h3")
+    p.add_argument("--decode", action="store_true", help="profile the decoder (dec(z_q, vq=False)) instead of encode + VQ")
     a = p.parse_args()
     L.set_precision(a.precision)
     import bench
@@ -62,6 +63,21 @@ def main():
         rows.append((f"ResLSTM H={H} T={T} layers={self.lstm.num_layers}", fl, e0, e1))
         return y
 
+    torig = CV.ConvTranspose1dWN.run
+
+    def timed_convt(self, x, out_snake=None, dual=False):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = torig(self, x, out_snake, dual)
+        y = out[0] if dual else out
+        e1.record()
+        B, Cin, T = x.shape
+        fl = 2.0 * B * self.out_channels * Cin * self.kernel_size * T
+        rows.append((f"convT Cin={Cin} Cout={self.out_channels} k={self.kernel_size} s={self.stride} T={y.shape[-1]}"
+                     f"{' snake' if out_snake is not None else ''}", fl, e0, e1))
+        return out
+
     rorig = BLK.ResidualUnit._flow_fused
 
     def timed_ru(self, cfg, x_raw, x_act, want_raw, next_act):
@@ -77,15 +93,21 @@ def main():
         return out
 
     with torch.no_grad():
-        dec(enc(x), vq=True)  # warm-up / weight prep
+        zq = dec(enc(x), vq=True)[0]  # warm-up / weight prep
+        if a.decode:
+            dec(zq, vq=False)
         torch.cuda.synchronize()
         CV.Conv1dWN.run = timed_run
+        CV.ConvTranspose1dWN.run = timed_convt
         BLK.ResLSTM.run = timed_lstm
         BLK.ResidualUnit._flow_fused = timed_ru
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        dec(enc(x), vq=True)
+        if a.decode:
+            dec(zq, vq=False)
+        else:
+            dec(enc(x), vq=True)
         e1.record()
         torch.cuda.synchronize()
     total = e0.elapsed_time(e1)
