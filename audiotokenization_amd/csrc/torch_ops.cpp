@@ -114,13 +114,13 @@ std::vector<Tensor> conv_transpose1d(const Tensor& x, at::TensorList w_phases, c
   // per-phase contiguous rows + one interleave pass (bc_convT1d_fwd_ws): the same values as the strided-store path
   const long long nws = bc_convT1d_workspace_floats(i32(B, "B"), i32(cout, "Cout"), i32(tout, "Tout"), i32(k, "K"),
                                                     i32(stride, "stride"), i32(padding, "padding"), dual ? 1 : 0);
-  TORCH_CHECK_VALUE(nws >= 0, "bigcodec::conv_transpose1d: bad shape for the workspace query");
+  // nws < 0: a stride beyond the interleave's table (> 16): the strided-store path, no workspace
   auto ws = at::empty({(int64_t)(nws > 0 ? nws : 1)}, x.options());
   ok(bc_convT1d_fwd_ws(x.data_ptr<float>(), ph.data(), optf(x, bias, "bias"), optf(x, sa, "snake_alpha_exp"),
                        optf(x, sb, "snake_inv_beta"), y.data_ptr<float>(), dual ? y2.data_ptr<float>() : nullptr,
                        i32(B, "B"), i32(x.size(1), "Cin"), i32(x.size(2), "T"), i32(cout, "Cout"), i32(tout, "Tout"),
-                       i32(k, "K"), i32(stride, "stride"), i32(padding, "padding"), i32(cfg, "cfg"), ws.data_ptr<float>(),
-                       stream_of(x)),
+                       i32(k, "K"), i32(stride, "stride"), i32(padding, "padding"), i32(cfg, "cfg"),
+                       nws >= 0 ? ws.data_ptr<float>() : nullptr, stream_of(x)),
      "bc_convT1d_fwd_ws");
   if (dual) return {y, y2};
   return {y};
