@@ -143,6 +143,10 @@ static int w16(int bit, int tile8, int tile16) { return (x6_w16() & bit) ? tile1
 
 static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
+  // Cout = 1 (the decoder's last conv, 48 -> 1, k7): the 16 x 256 tile (two taps per K-step over the double B buffer)
+  // instead of the 16 x 128 two-per-CU tile 113: half the workgroups of a conv with one output row, 2.83 -> 1.73 ms at
+  // B = 64 x 240 000 (profiles/r03y_cout1.txt)
+  if (Cout == 1 && s == 1 && x6_ncol(kX6Tiles[8], K, 1, d) <= 32 * X6_MAXCOL_ITERS) return 108;
   if (s == 1 && K == 1) {
     if (Cout >= 2048 && Cout % 192 == 0 && (x6_w16() & 16)) return 122;
     if (Cout >= 2048 && Cout % 256 == 0) return 121;
