@@ -114,13 +114,20 @@ def call(name: str, *args) -> int:
     return rc
 
 
-_pending_status = []  # (device int32 status tensor, what) of launches not yet checked
+_tls = threading.local()  # per-thread status state: concurrent forwards on two threads never mix their words
+
+
+def _pending():
+    p = getattr(_tls, "pending", None)
+    if p is None:
+        p = _tls.pending = []
+    return p
 
 
 def defer_status(status, what: str) -> None:
     """Remember a device status word (nonzero = the launch failed, e.g. a persistent-kernel timeout,
     include/bigcodec.h) to be checked by check_status() before the caller's output is consumed."""
-    _pending_status.append((status, what))
+    _pending().append((status, what))
 
 
 @contextlib.contextmanager
@@ -129,31 +136,89 @@ def status_scope():
     list, the body ends with check_status(); when the body raises instead, its unchecked words are dropped
     with it (that forward's output is never consumed), so a later forward cannot raise for a batch that
     already failed (a stale status after a per-batch error in the extraction loops).  Scopes
-    nest: the enclosing forward's words are restored on exit."""
-    global _pending_status
-    outer, _pending_status = _pending_status, []
+    nest: the enclosing forward's words are restored on exit.  The list is per thread."""
+    outer = _pending()
+    _tls.pending = []
     try:
         yield
     finally:
-        _pending_status = outer
+        _tls.pending = outer
 
 
-def check_status() -> None:
-    """Read every pending status word (ONE device -> host copy, which waits for the stream) and raise
-    BigCodecLibraryError if any launch reported a failure.  Called at the end of each codec forward
-    (encoder, decoder, streaming push, standalone ResLSTM)."""
-    global _pending_status
-    if not _pending_status:
-        return
-    import torch
-
-    items, _pending_status = _pending_status, []
-    vals = torch.cat([t.reshape(-1) for t, _ in items]).cpu().tolist()
+def _raise_bad(items, vals) -> None:
     bad = [f"{what}: {v} workgroup(s) timed out" for (_, what), v in zip(items, vals) if v]
     if bad:
         raise BigCodecLibraryError("persistent LSTM launch failed, its output is wrong (" + "; ".join(bad) +
                                    "). The H/8 workgroups of the recurrence must be co-resident; another "
                                    "kernel holding CUs for seconds can starve them.")
+
+
+def check_status() -> None:
+    """Read every pending status word (ONE device -> host copy, which waits for the stream) and raise
+    BigCodecLibraryError if any launch reported a failure.  Called at the end of each codec forward
+    (encoder, decoder, streaming push, standalone ResLSTM).  Inside deferred_status() the words are handed
+    to that scope's StatusTicket instead, and nothing waits for the device."""
+    items = _pending()
+    if not items:
+        return
+    _tls.pending = []
+    coll = getattr(_tls, "deferred", None)
+    if coll is not None:
+        coll.extend(items)
+        return
+    import torch
+
+    _raise_bad(items, torch.cat([t.reshape(-1) for t, _ in items]).cpu().tolist())
+
+
+class StatusTicket:
+    """The status words of the forwards run inside one deferred_status() scope, copied to pinned host memory
+    behind the scope's work on the stream (no wait).  ready() polls, check() waits for the copy and raises
+    BigCodecLibraryError like check_status() would have."""
+
+    def __init__(self):
+        self.items, self.host, self.event = [], None, None
+
+    def _arm(self, items) -> None:
+        import torch
+
+        self.items = items
+        if not items:
+            return
+        dev = items[0][0].device
+        if dev.type != "cuda":  # host words (CPU test doubles): nothing to wait for
+            self.host = torch.stack([t.reshape(-1)[0].to(torch.int32) for t, _ in items])
+            return
+        self.host = torch.empty(len(items), dtype=torch.int32, pin_memory=True)
+        for i, (t, _) in enumerate(items):  # copies only: no compute kernel on the product path
+            self.host[i:i + 1].copy_(t.reshape(-1)[:1].to(torch.int32), non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(dev))
+
+    def ready(self) -> bool:
+        return self.event is None or self.event.query()
+
+    def check(self) -> None:
+        if self.event is not None:
+            self.event.synchronize()
+        if self.host is not None:
+            _raise_bad(self.items, self.host.tolist())
+
+
+@contextlib.contextmanager
+def deferred_status():
+    """Run forwards without their end-of-forward status read (a host wait for the whole forward): the words
+    go to the yielded StatusTicket, armed when the body completes; the caller checks it before it uses the
+    outputs (extract.ShardedExtractor checks batch i while batch i + 1 is queued on the device)."""
+    items = []
+    outer = getattr(_tls, "deferred", None)
+    _tls.deferred = items
+    ticket = StatusTicket()
+    try:
+        yield ticket
+    finally:
+        _tls.deferred = outer
+    ticket._arm(items)
 
 
 def conv_cfg(Cout: int, Cin: int, K: int, stride: int, dilation: int, mode: int) -> int:
@@ -251,7 +316,7 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
                                               (4, 1, 1, 8), (3, 1, 1, 8), (2, 1, 1, 8), (1, 1, 1, 8),
                                               (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4),
                                               (8, 2, 2, 4), (4, 4, 4, 2), (6, 4, 2, 4), (8, 4, 2, 4),
-                                              (6, 2, 2, 8),  # 122: 16 waves, h3 and bf16
+                                              (6, 2, 2, 8),  # 122: 16 waves (h3, bf16 and x6)
                                               (3, 2, 2, 4), (3, 4, 1, 8)])}  # 123, 124: one-launch ResidualUnit only
 
 
@@ -284,7 +349,7 @@ def resunit_kernel_name(cfg: int, C: int = 0, dilation: int = 1) -> str:
 
 # Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6":
 # same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
-# 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the LSTM stays fp32-accurate),
+# 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the ResLSTM runs on h3: fp32-class, 22-bit operands),
 # 3 = "h3", the default: two fp16 planes per operand with power-of-two block scaling, three products
 # (fp32-class accuracy, measured below the fp32 MFMA kernel's error) at half the x6
 # MFMA count.

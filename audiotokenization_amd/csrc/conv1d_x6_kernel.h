@@ -226,7 +226,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       // fresh reads before every m-tile
       // (multi-tap tiles with NT > 1 and at most 24 accumulator tiles: the extra register set spills
       // in the others)
-      constexpr bool APF = !PW && NT > 1 && MT * NT <= 24;
+      // (x6 on the 16-wave tile: its three planes leave no room for the second set, 41 spilled VGPRs with it)
+      constexpr bool APF = !PW && NT > 1 && MT * NT <= 24 && !(P == 3 && WM * WN == 16);
       frag_t af[2][P];
       auto load_a = [&](int i, frag_t (&d)[P]) {
         const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
@@ -535,17 +536,12 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   return BC_OK;
 }
 
-// the 16-wave tile (h3 and bf16; the x6 planes do not fit its 128 VGPRs, so no x6 instances are compiled).  Measured and not kept
-// (profiles/r02g_w16_tiles.txt, r02g_w16b.txt): 48 x 64 per wave (111 spilled VGPRs, 2.5x slower) and a
-// 256 x 256 tile of 128 x 32 per wave (86-136 spilled VGPRs, 2.2-2.6x slower).
+// the 16-wave tile (every precision; x6 runs it without the A-fragment prefetch, which leaves 1 spilled VGPR
+// at 128).  Measured and not kept (profiles/r02g_w16_tiles.txt, r02g_w16b.txt): 48 x 64 per wave (111 spilled
+// VGPRs, 2.5x slower) and a 256 x 256 tile of 128 x 32 per wave (86-136 spilled VGPRs, 2.2-2.6x slower).
 template <int P>
 static int launch_x6_w16(ConvArgs& a, int B, hipStream_t st) {
-  if constexpr (P <= 2) {
-    return launch_x6<6, 2, 2, 8, P>(a, B, st);
-  } else {
-    (void)a, (void)B, (void)st;
-    return BC_ERR_UNSUPPORTED;
-  }
+  return launch_x6<6, 2, 2, 8, P>(a, B, st);
 }
 
 // launch tile index `tile` (kX6Tiles) with P operand planes; instantiated in conv1d_x6_p<P>.hip

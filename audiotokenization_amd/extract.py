@@ -3,12 +3,14 @@
   * index post-processing and on-disk format (extract_indices.py:512-561): codes (Nq, 1, F) ->
     squeeze(1) -> permute to (F, Nq) -> int16 -> np.save(<out>/<subset>/<spk>/<chapter>/<fileid>.npy)
   * clip-sharded data-parallel extraction: global clip ids are block-partitioned
-    over ranks, each rank encodes its own batches, and the batch's int64 index tensor is
-    all-gathered over the process group (RCCL over xGMI on MI355X, gloo on CPU test runs).
+    over ranks, each rank encodes its own batches, and the batch's index tensor is all-gathered as
+    int16 over the process group (RCCL over xGMI on MI355X, gloo on CPU test runs); the per-batch status
+    table travels over a host-side gloo group, so no host waits for an encode while its device idles.
   * per-item error accounting (extract_indices.py:565-574): failures are counted, not fatal.
 """
 from __future__ import annotations
 
+import collections
 import os
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Tuple
@@ -246,11 +248,17 @@ class ShardedExtractor:
     rank runs the same number of batches (the last ones padded with clip ids that are discarded), so
     the per-batch collectives line up.  A batch whose source or model raises is counted, not fatal
     (extract_indices.py:565-574) — and the failing rank STILL joins both of the batch's collectives:
-    first an all-gather of (ok, Nq, F) per rank, then, if any rank succeeded, the all-gather of the
-    (Nq, B, F) codes as int16 (the on-disk type, extract_indices.py:532), in which a failed rank contributes
-    zeros of the agreed shape.  The agreed shape comes from the status table every rank holds
+    first an all-gather of (ok, Nq, F, real clips) per rank, then, if any rank succeeded, the all-gather of
+    the (Nq, B, F) codes as int16 (the on-disk type, extract_indices.py:532), in which a failed rank
+    contributes zeros of the agreed shape.  The agreed shape comes from the status table every rank holds
     (agreed_shape), so a rank whose codes have another shape is counted as failed on every rank alike
     and no rank can be left waiting in a collective another rank skipped.
+
+    Nothing on the host waits for a batch's encode while the device is idle: step(i) queues batch i's
+    encode with its status words deferred (_lib.deferred_status), and only then finishes batch i - `depth`
+    (reads its status words — the device is busy with batch i meanwhile —, exchanges the status table over a
+    host-side gloo group, queues the codes all-gather over the device group, RCCL on MI355X, and hands the
+    codes to the sink).  flush() finishes every queued batch.
 
     `source(clip0, n) -> (n, 1, T)` supplies a batch (default: bc_synth_clips on `device`);
     `model(x)` returns the codes (Nq, B, F) or a dict with "indices" (BigCodecModel);
@@ -259,11 +267,13 @@ class ShardedExtractor:
     D2H copy and the sink overlap the next batches); run() / flush() wait for it."""
 
     def __init__(self, model, n_clips: int, n_samples: int, batch: int, rank: int = 0, world: int = 1,
-                 device=None, gather: bool = True, sink=None, group=None, source=None, sink_depth: int = 4):
-        if batch <= 0 or n_clips < 0:
-            raise ValueError("batch must be > 0 and n_clips >= 0")
+                 device=None, gather: bool = True, sink=None, group=None, source=None, sink_depth: int = 4,
+                 depth: int = 1):
+        if batch <= 0 or n_clips < 0 or depth < 0:
+            raise ValueError("batch must be > 0, n_clips >= 0 and depth >= 0")
         self.model, self.n_clips, self.n_samples, self.batch = model, n_clips, n_samples, batch
         self.rank, self.world, self.gather, self.sink, self.group = rank, world, gather, sink, group
+        self.depth = depth
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.source = source or (lambda clip0, n: synth_batch(n, n_samples, clip0, self.device))
         self.lo, self.hi = shard_range(n_clips, rank, world)
@@ -272,26 +282,53 @@ class ShardedExtractor:
         self.stats = ExtractStats()
         self.writer = _SinkWriter(sink, sink_depth) if (rank == 0 and sink is not None) else None
         self.last = None  # rank 0: the last batch's gathered (W, Nq, B, F) int16 host tensor (filled behind the device)
+        self.queued = collections.deque()  # batches encoded (queued on the device) but not finished yet
+        self.ctl = self._control_group() if (gather and world > 1) else None
+
+    def _control_group(self):
+        """The host-side group of the status exchange: the device group itself when it is gloo, else a gloo
+        group over the same ranks (every rank constructs the extractor, so every rank creates it)."""
+        import torch.distributed as dist
+
+        if not dist.is_available() or not dist.is_initialized():
+            return None
+        if dist.get_backend(self.group) == "gloo":
+            return self.group
+        ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
+        return dist.new_group(ranks=ranks, backend="gloo")
 
     def step(self, bi: int):
-        """Batch `bi` of every rank: encode, gather, queue for the sink.  Returns the gathered
-        (W, Nq, B, F) int16 device codes, or None when the batch failed on every rank."""
-        st = self.stats
+        """Queue batch `bi` of every rank on the device, then finish the batches beyond the pipeline depth.
+        Returns the gathered (W, Nq, B, F) int16 device codes of the last batch finished here, or None (no
+        batch finished, or it failed on every rank)."""
         s = self.lo + bi * self.batch
         real = max(0, min(s + self.batch, self.hi) - s)
-        codes = None
+        codes = ticket = None
         try:
-            codes = _codes_of(self.model(self.source(s, self.batch)))
+            with L.deferred_status() as ticket:
+                codes = _codes_of(self.model(self.source(s, self.batch)))
             if codes.ndim != 3 or codes.shape[1] != self.batch:
                 raise ValueError(f"model returned codes of shape {tuple(codes.shape)}, expected (Nq, {self.batch}, F)")
         except Exception:  # per-batch accounting, mirrors extract_indices.py:565-574
             codes = None
+        self.queued.append((bi, s, real, codes, ticket))
+        out = None
+        while len(self.queued) > self.depth:
+            out = self._finish(*self.queued.popleft())
+        return out
+
+    def _finish(self, bi, s, real, codes, ticket):
+        st = self.stats
+        if codes is not None:
+            try:
+                ticket.check()  # the batch's persistent-LSTM status words (waits for this batch only)
+            except Exception:
+                codes = None
         st.batches += 1
         gather = self.gather and self.world > 1
-        dev = codes.device if codes is not None else self.device
         status = torch.tensor([1 if codes is not None else 0, codes.shape[0] if codes is not None else 0,
                                codes.shape[2] if codes is not None else 0, real], dtype=torch.int64)
-        stat = all_gather_status(status.to(dev), self.group).cpu() if gather else status.unsqueeze(0)
+        stat = all_gather_status(status, self.ctl) if gather else status.unsqueeze(0)
         agreed = agreed_shape(stat)
         keep = agreed[2] if agreed is not None else torch.zeros(stat.shape[0], dtype=torch.bool)
         me = self.rank if gather else 0
@@ -307,7 +344,7 @@ class ShardedExtractor:
         if agreed is None:
             return None
         nq, nf = agreed[0], agreed[1]
-        codes16 = (torch.zeros((nq, self.batch, nf), dtype=torch.int16, device=dev) if codes is None
+        codes16 = (torch.zeros((nq, self.batch, nf), dtype=torch.int16, device=self.device) if codes is None
                    else codes.to(torch.int16))  # extract_indices.py:532's astype(np.int16), on the device
         gathered = all_gather_codes(codes16, self.group) if gather else codes16.unsqueeze(0)
         if self.writer is not None:
@@ -322,23 +359,40 @@ class ShardedExtractor:
         return gathered
 
     def flush(self):
-        """Wait until the sink has received every batch stepped so far (re-raises a sink error)."""
+        """Finish every queued batch, then wait until the sink has received them (re-raises a sink error).
+        Returns the gathered codes of the last batch finished, or None."""
+        out = None
+        while self.queued:
+            out = self._finish(*self.queued.popleft())
         if self.writer is not None:
             self.writer.flush()
+        return out
 
     def close(self):
-        if self.writer is not None:
-            self.writer.flush()
-            self.writer.close()
-            self.writer = None
+        """Stop the writer thread (after it has drained; a sink error is re-raised once it has stopped).
+        Batches still queued are not finished: flush() first on the success path."""
+        w, self.writer = self.writer, None
+        if w is not None:
+            try:
+                w.flush()
+            finally:
+                w.close()
 
     def run(self) -> ExtractStats:
+        ok = False
         try:
             for bi in range(self.n_batches):
                 self.step(bi)
             self.flush()
+            ok = True
         finally:
-            self.close()
+            if ok:
+                self.close()
+            else:  # the original exception propagates; a sink error behind it must not replace it
+                try:
+                    self.close()
+                except Exception:
+                    pass
         return self.stats
 
 

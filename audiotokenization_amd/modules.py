@@ -149,7 +149,8 @@ class Snake(SnakeBeta):
 
 
 # Adopted, as the reference's vq/alias_free_torch/filter.py:25-27 states for its own copy, from adefossez's
-# julius.lowpass.LowPassFilters under the MIT License (https://adefossez.github.io/julius/julius/lowpass.html).
+# julius.lowpass.LowPassFilters under the MIT License (https://adefossez.github.io/julius/julius/lowpass.html);
+# the reference's filter.py:1-2 credits the alias-free-torch package (junjun3518) under the Apache License 2.0.
 # The buffer values must be bit-identical to the reference's (test_oracle_pinned.py), hence the same expression.
 def kaiser_sinc_filter1d(cutoff, half_width, kernel_size):
     """vq/alias_free_torch/filter.py:28-57 (init-time constant; returns (1,1,kernel_size))."""

@@ -97,6 +97,35 @@ def kernel_table(summ, steps, probe, n=8):
     return rows
 
 
+def roofline(summ, steps, probe):
+    """The `roofline` object of the JSON line: the dominant HIP-event-timed kernel (largest total time over the
+    timed steps), its algorithmic TFLOP/s at its average launch duration against its MFMA ceiling (spec and
+    probe-measured), the newest committed PMC traffic / MFMA utilisation of that kernel, and kernels_top."""
+    kname, d = max(summ.items(), key=lambda kv: kv[1]["ms_total"])
+    avg_ms = d["ms_total"] / d["launches"]
+    achieved = d["flops_total"] / d["launches"] / (avg_ms * 1e-3) / 1e12
+    conv_ms = sum(v["ms_total"] for v in summ.values())
+    traffic, mutil, tsrc = pmc_traffic(kname)
+    peak, mult, note = kernel_peak(kname)
+    practical = probe / mult if kname.startswith("conv1d_x6_kernel") else None
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "peak_note": note,
+            "probe_bf16_tflops": round(probe, 1),
+            "practical_peak": round(practical, 2) if practical else None,
+            "practical_frac": round(achieved / practical, 4) if practical else None,
+            "practical_note": "bc_mfma_probe: the dense-BF16 rate this device sustains on random register "
+                              "operands (its clock under MFMA load), / the kernel's MFMAs per FLOP pair",
+            "mfma_tflops_executed": round(achieved * mult, 2),
+            "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
+            "pmc_mfma_util": round(mutil, 4) if mutil is not None else None,
+            "algorithmic_bytes_per_launch": round(d["bytes_total"] / d["launches"]), "kernel": kname,
+            "launches_per_step": d["launches"] // steps, "avg_launch_ms": round(avg_ms, 4),
+            "algorithmic_gflop_per_launch": round(d["flops_total"] / d["launches"] / 1e9, 3),
+            "all_python_conv_kernels_ms_per_step": round(conv_ms / steps, 2),
+            "all_python_conv_tflops": round(sum(v["flops_total"] for v in summ.values()) / (conv_ms * 1e-3) / 1e12, 2),
+            "kernels_top": kernel_table(summ, steps, probe)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -454,33 +483,11 @@ def main():
 
     audio_s = world * B * n_samples / args.sample_rate * args.steps
     value = audio_s / elapsed
+    probe = None
     roof = None
     if timer is not None:
-        summ = timer.summary()
-        kname, d = max(summ.items(), key=lambda kv: kv[1]["ms_total"])
-        avg_ms = d["ms_total"] / d["launches"]
-        achieved = d["flops_total"] / d["launches"] / (avg_ms * 1e-3) / 1e12
-        conv_ms = sum(v["ms_total"] for v in summ.values())
-        traffic, mutil, tsrc = pmc_traffic(kname)
-        peak, mult, note = kernel_peak(kname)
         probe = mfma_probe_tflops(dev)
-        practical = probe / mult if kname.startswith("conv1d_x6_kernel") else None
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "peak_note": note,
-                "probe_bf16_tflops": round(probe, 1),
-                "practical_peak": round(practical, 2) if practical else None,
-                "practical_frac": round(achieved / practical, 4) if practical else None,
-                "practical_note": "bc_mfma_probe: the dense-BF16 rate this device sustains on random register "
-                                  "operands (its clock under MFMA load), / the kernel's MFMAs per FLOP pair",
-                "mfma_tflops_executed": round(achieved * mult, 2),
-                "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
-                "pmc_mfma_util": round(mutil, 4) if mutil is not None else None,
-                "algorithmic_bytes_per_launch": round(d["bytes_total"] / d["launches"]), "kernel": kname,
-                "launches_per_step": d["launches"] // args.steps, "avg_launch_ms": round(avg_ms, 4),
-                "algorithmic_gflop_per_launch": round(d["flops_total"] / d["launches"] / 1e9, 3),
-                "all_python_conv_kernels_ms_per_step": round(conv_ms / args.steps, 2),
-                "all_python_conv_tflops": round(sum(v["flops_total"] for v in summ.values()) / (conv_ms * 1e-3) / 1e12, 2),
-                "kernels_top": kernel_table(summ, args.steps, probe)}
+        roof = roofline(timer.summary(), args.steps, probe)
 
     # rank 0's own batch codes (Nq, B, F) of the last timed step, for parity
     mine = None
@@ -496,12 +503,14 @@ def main():
         _lib.set_precision("x6")
         for _ in range(1):
             step()
-        el6, codes6 = timed(args.x6_steps)
+        timer6 = None if args.no_kernel_timer else _lib.KernelTimer()
+        el6, codes6 = timed(args.x6_steps, timer6)
         _lib.set_precision(args.precision)
         v6 = world * B * n_samples / args.sample_rate * args.x6_steps / el6
         x6 = {"precision": "x6: fp32 operands split exactly into 3 bf16 terms, 6 bf16 MFMAs per product, fp32 "
                            "accumulate (24-bit operands)",
-              "value": round(v6, 2), "ms_per_step": round(el6 / args.x6_steps * 1e3, 2), "steps": args.x6_steps}
+              "value": round(v6, 2), "ms_per_step": round(el6 / args.x6_steps * 1e3, 2), "steps": args.x6_steps,
+              "roofline": roofline(timer6.summary(), args.x6_steps, probe) if timer6 is not None else None}
         if rank == 0:
             x6["parity"] = golden_parity((codes6[0] if world > 1 else codes6)[:, :B], args.model, n_samples, B)
 
@@ -552,7 +561,7 @@ def main():
                        "fp32-class: operands block-scaled and split into 2 fp16 terms (22-bit), 3 fp16 "
                        "MFMAs per product (lo x lo dropped, < 2^-22 relative), fp32 accumulate"),
                 "bf16": ("bf16", "bf16 conv products (one bf16 MFMA per product), fp32 accumulate and storage; "
-                                 "LSTM and VQ fp32-accurate")}[args.precision]
+                                 "ResLSTM on h3 (fp32-class, 22-bit operands), VQ fp32 (IEEE op order)")}[args.precision]
         line = {
             "metric": METRIC_RT if cfgn == 3 else METRIC_DEC if cfgn == 6 else METRIC, "value": round(value, 2),
             "unit": "audio-sec/s",

@@ -20,7 +20,8 @@ def pytest_configure(config):
 # whole-model test trips over it), the full-size config runs last (they take the longest).  Stable: the
 # order within a module is unchanged; modules not listed keep their place before the listed ones.
 _GPU_ORDER = ["test_gpu_kernels", "test_gpu_ops", "test_gpu_fsq", "test_gpu_model", "test_gpu_tokens",
-              "test_gpu_streaming", "test_gpu_extract", "test_extract_cli", "test_gpu_full_size"]
+              "test_gpu_streaming", "test_gpu_extract", "test_extract_cli", "test_gpu_full_size",
+              "test_gpu_configs"]
 
 
 def pytest_collection_modifyitems(config, items):

@@ -238,3 +238,76 @@ def test_sink_errors_surface():
     with pytest.raises(OSError, match="disk full"):
         extract_sharded(lambda x: _fake_codes(x[:, 0, 0].long()), 7, 8, 3, device=torch.device("cpu"), sink=bad_sink,
                         source=_fake_source)
+
+
+def test_extract_pipeline_finishes_batch_i_after_queueing_i_plus_1():
+    """step(i) queues batch i, then finishes batch i - depth (its status read waits for that batch only, while
+    batch i is already queued on the device); flush() finishes the rest.  depth = 0 finishes every batch in
+    its own step."""
+    from audiotokenization_amd.extract import ShardedExtractor
+
+    log = []
+
+    def model(x):
+        log.append(("encode", int(x[0, 0, 0])))
+        return _fake_codes(x[:, 0, 0].long())
+
+    def sink(cid, arr):
+        log.append(("sink", cid))
+
+    ex = ShardedExtractor(model, 7, 8, 3, device=torch.device("cpu"), sink=sink, source=_fake_source, depth=1)
+    assert ex.step(0) is None  # queued only
+    g0 = ex.step(1)  # batch 0 finished after batch 1 was queued
+    assert g0 is not None and g0.shape == (1, NQ, 3, NF) and g0[0, 0, :, 0].tolist() == [0, 100, 200]
+    g1 = ex.step(2)
+    assert g1[0, 0, :, 0].tolist() == [300, 400, 500]
+    g2 = ex.flush()
+    assert g2[0, 0, :, 0].tolist() == [600, 700, 800]  # clips 7, 8 pad the last batch (encoded, never sunk)
+    ex.close()
+    enc = [c for k, c in log if k == "encode"]
+    assert enc == [0, 3, 6]
+    assert sorted(c for k, c in log if k == "sink") == list(range(7))
+    ex0 = ShardedExtractor(model, 7, 8, 3, device=torch.device("cpu"), source=_fake_source, depth=0)
+    assert ex0.step(0)[0, 0, :, 0].tolist() == [0, 100, 200]
+
+
+def test_extract_deferred_status_word_fails_its_batch():
+    """A persistent-kernel status word raised by a forward (deferred into the batch's StatusTicket) fails that
+    batch only: counted, not sunk, the other batches arrive (extract_indices.py:565-574)."""
+    from audiotokenization_amd import _lib as L
+    from audiotokenization_amd.extract import extract_sharded
+
+    calls = {"n": 0}
+
+    def model(x):
+        bi = calls["n"]
+        calls["n"] += 1
+        with L.status_scope():
+            L.defer_status(torch.tensor([3 if bi == 1 else 0], dtype=torch.int32), "ResLSTM(test)")
+            L.check_status()
+        return _fake_codes(x[:, 0, 0].long())
+
+    sunk = {}
+    st = extract_sharded(model, 7, 8, 3, device=torch.device("cpu"), sink=lambda cid, arr: sunk.__setitem__(cid, arr),
+                         source=_fake_source)
+    assert st.errors == 3 and st.error_items == [3, 4, 5] and st.clips == 4
+    assert sorted(sunk) == [0, 1, 2, 6]
+    with pytest.raises(L.BigCodecLibraryError, match="timed out"):  # outside the deferral the read raises at once
+        with L.status_scope():
+            L.defer_status(torch.tensor([1], dtype=torch.int32), "ResLSTM(test)")
+            L.check_status()
+
+
+def test_sink_error_stops_the_writer_thread():
+    """after a sink error the writer thread is stopped (sentinel + join), not left blocked."""
+    import threading
+
+    from audiotokenization_amd.extract import extract_sharded
+
+    def bad_sink(cid, arr):
+        raise OSError("disk full")
+
+    with pytest.raises(OSError, match="disk full"):
+        extract_sharded(lambda x: _fake_codes(x[:, 0, 0].long()), 7, 8, 3, device=torch.device("cpu"), sink=bad_sink,
+                        source=_fake_source)
+    assert not [t for t in threading.enumerate() if t.name == "bigcodec-sink" and t.is_alive()]

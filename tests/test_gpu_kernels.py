@@ -94,16 +94,17 @@ def test_conv1d(dev, case, prec):
     (768, 768, 7, 1, 9, 300, (320, 322)), (384, 768, 10, 5, 1, 300, (5320, 5322)),
     (192, 384, 4, 2, 1, 520, (2320, 2322)), (96, 192, 4, 2, 1, 600, (2320, 2322)),
     (768, 1536, 10, 5, 1, 130, (5320, 5322))])
-@pytest.mark.parametrize("tprec", ["h3", "bf16"])
+@pytest.mark.parametrize("tprec", ["h3", "bf16", "x6"])
 def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
     """The 192 x 256 h3 tile with 8 waves of 96 x 64 (cfg 320) and with 16 waves of 96 x 32 (322; the
     phase-decomposed strided convs as 1000 s + tile) stages the same B chunks with the same block scales
     and runs the same per-output MFMA chains: bit-identical outputs, and within the conv tolerance of the
-    oracle.  The bf16 planes (cfg - 100) run the same two tiles."""
+    oracle.  The bf16 planes (cfg - 100) and the x6 planes (cfg - 200: three bf16 planes, the 16-wave tile
+    without the A-fragment prefetch) run the same two tiles."""
     old = L.precision_mode()
     L.set_precision(tprec)
-    if tprec == "bf16":
-        cfgs = tuple(c - 100 for c in cfgs)
+    if tprec != "h3":
+        cfgs = tuple(c - (100 if tprec == "bf16" else 200) for c in cfgs)
     try:
         g = torch.Generator().manual_seed(Cin * 31 + Cout + d)
         pad = K // 2 * d if s == 1 else s // 2 + s % 2
@@ -125,7 +126,7 @@ def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
                    B, Cin, T, Cout, Tout, K, s, d, pad, 0, cfg, st)
             torch.cuda.synchronize()
             outs[cfg] = y.cpu()
-        tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if tprec == "h3" else 2e-2
+        tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if tprec != "bf16" else 2e-2
         assert_close_rel(outs[cfgs[0]], want, tol, f"{tprec} {cfgs[0]}")
         for c in cfgs[1:]:
             assert torch.equal(outs[c], outs[cfgs[0]]), (c, (outs[c] - outs[cfgs[0]]).abs().max())

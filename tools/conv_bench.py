@@ -11,7 +11,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# BIGCODEC_PKG_ROOT: import the package from another tree (e.g. an ablation build, tools/r03h_ablation.sh)
+# BIGCODEC_PKG_ROOT: import the package from another tree (e.g. an ablation build, tools/lab/r03h_ablation.sh)
 sys.path.insert(0, os.environ.get("BIGCODEC_PKG_ROOT", REPO))
 
 import torch  # noqa: E402
@@ -60,7 +60,7 @@ def main():
         tiles = [c + base for c in sorted(L.X6_CFGS)]
         cfgs = tiles + ([1000 * a.s + c for c in tiles] if a.s >= 2 else [])
     else:
-        cfgs = [int(c) for c in a.cfg.split(",") if c] or [chosen]
+        cfgs = [chosen if c == "c" else int(c) for c in a.cfg.split(",") if c] or [chosen]  # "c": the library's
     st = torch.cuda.current_stream().cuda_stream
     fl = 2.0 * a.B * a.cout * a.cin * a.k * Tout
     nb = 4.0 * (x.numel() + y.numel() * (1 + a.res + a.dual))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ stall breakdown of one conv shape (tools/conv_bench.py), one counter group per rocprofv3 pass:
-#   CONV_ARGS="--cin 192 --cout 192 --k 7 --d 3 --T 60000 --snake" bash tools/conv_pmc.sh
+#   CONV_ARGS="--cin 192 --cout 192 --k 7 --d 3 --T 60000 --snake" bash tools/lab/conv_pmc.sh
 set -u
 mkdir -p gpurun_out/cpmc
 export TMPDIR=/tmp

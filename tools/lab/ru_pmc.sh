@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ / traffic counters of one ResidualUnit launch shape (tools/ru_bench.py), one counter group per rocprofv3 pass:
-#   RU_ARGS="--C 48 --d 3 --T 240000 --lazy" bash tools/ru_pmc.sh
+#   RU_ARGS="--C 48 --d 3 --T 240000 --lazy" bash tools/lab/ru_pmc.sh
 set -u
 mkdir -p gpurun_out/rpmc
 export TMPDIR=/tmp

@@ -6,7 +6,7 @@ by stage, first in h3 (to leave h3 data in every reused workspace, as the GPU te
 requested precision, and reports per stage whether the output equals the first repeat bit for bit, and the latent of
 clip 0 against the reference fixture.
 
-usage: python tools/x6_race_probe.py [--repeats 6] [--precisions x6,h3]
+usage: python tools/lab/x6_race_probe.py [--repeats 6] [--precisions x6,h3]
 """
 from __future__ import annotations
 

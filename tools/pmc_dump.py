@@ -1,4 +1,4 @@
-"""Per-kernel means of every counter in rocprofv3 --pmc pass directories (tools/ru_pmc.sh, tools/conv_pmc.sh):
+"""Per-kernel means of every counter in rocprofv3 --pmc pass directories (tools/lab/ru_pmc.sh, tools/lab/conv_pmc.sh):
 
     python tools/pmc_dump.py gpurun_out/rpmc [kernel-substring]"""
 import collections
