@@ -43,7 +43,11 @@ namespace bc {
 // idle one during chunk c's K-steps (maxima published at step 1, split and stored at step 2 for h3 /
 // step 1 otherwise) instead of behind an extra barrier at the chunk's last step, so the staging VALU and
 // LDS writes overlap the other waves' MFMAs.
-template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false>
+// B4 (multi-tap launches of stride-1 convs without phase decomposition, Tin % 4 == 0, 16-B aligned rows): the
+// input chunk is read with 16-byte loads, each thread one channel pair x IT4 column quads (4 loads per thread on
+// the 16-wave tile instead of 12 single-float loads), staged into the same LDS image with the same block maxima:
+// outputs bit-identical to the single-float staging.
+template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false, bool B4 = false>
 // NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
 // one workgroup's epilogue stores and operand loads overlap the other's MFMAs.  WM * WN = 16: one
 // 1024-thread workgroup (four waves per SIMD, <= 128 VGPRs).
@@ -55,6 +59,10 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
   static_assert(NW == 8 || NW == 16, "512- or 1024-thread workgroups");
   constexpr int NCG = NW / 8;  // B staging column groups (16 channel pairs x 32 column lanes each)
   constexpr int CI = ((PW ? BN / 32 : X6_MAXCOL_ITERS) + NCG - 1) / NCG;  // 32-column B passes per thread
+  static_assert(!(B4 && PW), "16-byte staging is for the multi-tap path");
+  constexpr int NQI = 4 * NW;  // B4: column quads per iteration (NW / 2 quad blocks of 8, 2 pair blocks of 8)
+  constexpr int IT4 = ((32 * X6_MAXCOL_ITERS + 6) / 4 + NQI - 1) / NQI;  // B4 iterations: ncol + 3 <= 4 * NQI * IT4
+  constexpr int NBL = B4 ? 2 * IT4 : 2 * CI;  // B load instructions per thread and chunk (the counted waits)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
   __shared__ unsigned smax[2][NW];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
   typedef typename FragType<P>::type frag_t;
@@ -139,6 +147,44 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       v1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, o1, 0, 0));
     }
   };
+  // B4 geometry: channel pair p4 of the chunk, column quad q = it * NQI + qb4 = input times tq0 + 4q .. + 3 =
+  // tile columns 4q - r4 .. 4q - r4 + 3 (r4 = in0 mod 4, uniform per launch)
+  const int r4 = ((in0 % 4) + 4) % 4;
+  const int tq0 = in0 - r4;
+  const int nq4 = (ncol + r4 + 3) >> 2;
+  const int p4 = 8 * (wave & 1) + (lane & 7);
+  const int qb4 = 8 * (wave >> 1) + (lane >> 3);
+  floatx4 bq0[B4 ? IT4 : 1], bq1[B4 ? IT4 : 1];
+  auto load_b4 = [&](int chunk, floatx4 (&v0)[B4 ? IT4 : 1], floatx4 (&v1)[B4 ? IT4 : 1]) {
+    const int c0 = chunk * X6_BKC + 2 * p4;
+#pragma unroll
+    for (int it = 0; it < IT4; ++it) {
+      const int q = it * NQI + qb4;
+      const int t = tq0 + 4 * q;
+      const bool ok = q < nq4 && t >= 0 && t < a.Tin;  // Tin % 4 == 0: a quad is wholly inside or outside
+      // out of range: 0x80000000 > num_records (< 2^31), and the 16 bytes do not wrap the 32-bit offset
+      const unsigned o0 = (ok && c0 < a.Cin) ? (unsigned)((c0 * a.Tin + t) * 4) : 0x80000000u;
+      const unsigned o1 = (ok && c0 + 1 < a.Cin) ? (unsigned)(((c0 + 1) * a.Tin + t) * 4) : 0x80000000u;
+      v0[it] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
+      v1[it] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o1, 0, 0));
+    }
+  };
+  auto bmax_publish4 = [&](const floatx4 (&w0)[B4 ? IT4 : 1], const floatx4 (&w1)[B4 ? IT4 : 1], int par) {
+    unsigned m = 0;  // over the tile's columns only (a quad's other times are not part of the staged tile)
+#pragma unroll
+    for (int it = 0; it < IT4; ++it) {
+      const int col0 = 4 * (it * NQI + qb4) - r4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool in = col0 + j >= 0 && col0 + j < ncol;
+        const unsigned u0 = in ? __float_as_uint(fabsf(w0[it][j])) : 0u, u1 = in ? __float_as_uint(fabsf(w1[it][j])) : 0u;
+        m = m > u0 ? m : u0;
+        m = m > u1 ? m : u1;
+      }
+    }
+    m = wave_max_u32(m);
+    if (lane == 0) smax[par][wave] = m;
+  };
   // P == 2: publish this wave's block maximum of a chunk's staged values / read the block's scale
   auto bmax_publish = [&](const float (&w0)[CI], const float (&w1)[CI], int par) {
     unsigned m = 0;
@@ -158,33 +204,55 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
   };
   float xs = 1.f;  // P == 2: scale of the staged chunk and of the accumulator
+  // channel pair pp of column col: split and stored into the P planes
+  auto put = [&](int col, int pp, float v0, float v1, unsigned char* Bt, float sc) {
+    unsigned char* p = Bt + bgrp(col, pp >> 2) + (pp & 3) * 4;
+    if constexpr (P == 2) {
+      unsigned h, m;
+      split2_h(v0 * sc, v1 * sc, h, m);
+      *reinterpret_cast<unsigned*>(p) = h;
+      *reinterpret_cast<unsigned*>(p + bplane) = m;
+      return;
+    }
+    const unsigned h = pk_bf16(v0, v1);
+    *reinterpret_cast<unsigned*>(p) = h;
+    if (P == 3) {
+      const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
+      const unsigned m = pk_bf16(r0, r1);
+      const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
+      const unsigned l = pk_bf16(s0, s1);
+      *reinterpret_cast<unsigned*>(p + bplane) = m;
+      *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
+    }
+  };
   auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI], unsigned char* Bt, float sc) {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
       const int col = bcol(i);
-      if (col < ncol) {
-        const float v0 = w0[i], v1 = w1[i];
-        if constexpr (P == 2) {
-          unsigned h, m;
-          split2_h(v0 * sc, v1 * sc, h, m);
-          unsigned char* p = Bt + bgrp(col, bp >> 2) + (bp & 3) * 4;
-          *reinterpret_cast<unsigned*>(p) = h;
-          *reinterpret_cast<unsigned*>(p + bplane) = m;
-          continue;
-        }
-        const unsigned h = pk_bf16(v0, v1);
-        unsigned char* p = Bt + bgrp(col, bp >> 2) + (bp & 3) * 4;
-        *reinterpret_cast<unsigned*>(p) = h;
-        if (P == 3) {
-          const float r0 = v0 - bf_lo(h), r1 = v1 - bf_hi(h);
-          const unsigned m = pk_bf16(r0, r1);
-          const float s0 = r0 - bf_lo(m), s1 = r1 - bf_hi(m);
-          const unsigned l = pk_bf16(s0, s1);
-          *reinterpret_cast<unsigned*>(p + bplane) = m;
-          *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
-        }
-      }
+      if (col < ncol) put(col, bp, w0[i], w1[i], Bt, sc);
     }
+  };
+  auto store_b4 = [&](const floatx4 (&w0)[B4 ? IT4 : 1], const floatx4 (&w1)[B4 ? IT4 : 1], unsigned char* Bt, float sc) {
+#pragma unroll
+    for (int it = 0; it < IT4; ++it) {
+      const int col0 = 4 * (it * NQI + qb4) - r4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (col0 + j >= 0 && col0 + j < ncol) put(col0 + j, p4, w0[it][j], w1[it][j], Bt, sc);
+    }
+  };
+  // the staging steps on whichever register set the variant uses
+  auto stage_load = [&](int chunk) {
+    if constexpr (B4) load_b4(chunk, bq0, bq1);
+    else load_b(chunk, bv0, bv1);
+  };
+  auto stage_max = [&](int par) {
+    if constexpr (B4) bmax_publish4(bq0, bq1, par);
+    else bmax_publish(bv0, bv1, par);
+  };
+  auto stage_store = [&](unsigned char* Bt, float sc) {
+    if constexpr (B4) store_b4(bq0, bq1, Bt, sc);
+    else store_b(bv0, bv1, Bt, sc);
   };
 
   floatx4 acc[MT][NT];
@@ -287,13 +355,13 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
 
   // prologue: A(step 0), B(chunk 0)
   issue_a(0, 0);
-  load_b(0, bv0, bv1);
+  stage_load(0);
   if constexpr (P == 2) {
-    bmax_publish(bv0, bv1, 0);
+    stage_max(0);
     lds_barrier();
     xs = bmax_scale(0);
   }
-  store_b(bv0, bv1, Bs, xs);
+  stage_store(Bs, xs);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -335,7 +403,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
         if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
         if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) {
           dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
-          load_b(c + 1, bv0, bv1);
+          stage_load(c + 1);
         }
         if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -347,27 +415,27 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
         if constexpr (DB) {
           // the idle buffer was last read in chunk c - 1 (every wave passed chunk c's first barrier)
           if (c + 1 < a.nchunks) {
-            if (P == 2 && tp == 1) bmax_publish(bv0, bv1, (c + 1) & 1);  // read at step 2, after a barrier
+            if (P == 2 && tp == 1) stage_max((c + 1) & 1);  // read at step 2, after a barrier
             if (tp == DB_STORE) {
               if constexpr (P == 2) {
                 const float sn = bmax_scale((c + 1) & 1);
                 xn = sn < xs ? sn : xs;
               }
-              if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1, Bs + ((c + 1) & 1) * P * bplane, xn);
+              if (!BC_ABL(a.dbg, 4)) stage_store(Bs + ((c + 1) & 1) * P * bplane, xn);
             }
           }
         } else if (tp == kst - 1 && c + 1 < a.nchunks) {
-          if constexpr (P == 2) bmax_publish(bv0, bv1, (c + 1) & 1);
+          if constexpr (P == 2) stage_max((c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
           if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-          if (!BC_ABL(a.dbg, 4)) store_b(bv0, bv1, Bs, xs);
+          if (!BC_ABL(a.dbg, 4)) stage_store(Bs, xs);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
-        // step 0 of a multi-step chunk the 2*CI B loads of the next chunk were issued after it and
+        // step 0 of a multi-step chunk the NBL B loads of the next chunk were issued after it and
         // may stay in flight (vmcnt retires in issue order); they are consumed at the chunk's last
         // step, where the compiler waits for their registers itself.
         if (tp == 0 && kst > 1 && c + 1 < a.nchunks)
-          wait_vmcnt<2 * CI>();
+          wait_vmcnt<NBL>();
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
@@ -463,17 +531,27 @@ inline bool x6_tps4_on() {
   return v;
 }
 
+// BC_X6_B4=0 keeps the single-float input staging everywhere (A/B timing).
+inline bool x6_b4_on() {
+  static const bool v = [] {
+    const char* e = getenv("BC_X6_B4");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 struct X6Variant {
   bool pw;
   int tps;
   bool db;
   size_t lds;
+  bool b4;  // 16-byte input staging (the launch also needs Tin % 4 == 0 and 16-B aligned rows, x6_b4_fits)
 };
-inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
+inline X6Variant x6_variant_base(const X6Tile& t, int P, int K, int s, int d) {
   const int ncol = x6_ncol(t, K, s, d);
   const size_t budget = t.NT > 1 ? 160 * 1024 : 80 * 1024;  // NT == 1: two workgroups per CU
   auto fits = [&](int tps, int bb) { return x6_lds(t, ncol, P, s, tps, bb) <= budget; };
-  if (K == 1 && ncol == x6_BN(t) && x6_pw_on()) return {true, 1, false, x6_lds(t, ncol, P, s)};
+  if (K == 1 && ncol == x6_BN(t) && x6_pw_on()) return {true, 1, false, x6_lds(t, ncol, P, s), false};
   const int min_kst = P == 2 ? 3 : 2;  // DB needs the store step after the maxima step
   // preference (profiles/r02_x6_db.txt): two taps per K-step over the double B buffer (fewer barriers
   // beat hidden staging: 192 x 256 k7 runs 2-3 % faster with TPS 2 than with DB at TPS 1); DB where only
@@ -483,11 +561,20 @@ inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d) {
   // bf16 on the 16-wave tile: one product per pair makes a two-tap K-step a third of h3's, too short to hide
   // the next step's A copy and the barrier; four taps per K-step over the double B buffer (k7: 2 K-steps per chunk)
   if (P == 1 && t.WM * t.WN == 16 && db && tps2 && x6_tps4_on() && (K + 3) / 4 >= min_kst && fits(4, 2))
-    return {false, 4, true, x6_lds(t, ncol, P, s, 4, 2)};
-  if (db && tps2 && (K + 1) / 2 >= min_kst && fits(2, 2)) return {false, 2, true, x6_lds(t, ncol, P, s, 2, 2)};
-  if (tps2 && fits(2, 1)) return {false, 2, false, x6_lds(t, ncol, P, s, 2)};
-  if (db && K >= min_kst && fits(1, 2)) return {false, 1, true, x6_lds(t, ncol, P, s, 1, 2)};
-  return {false, 1, false, x6_lds(t, ncol, P, s)};
+    return {false, 4, true, x6_lds(t, ncol, P, s, 4, 2), false};
+  if (db && tps2 && (K + 1) / 2 >= min_kst && fits(2, 2)) return {false, 2, true, x6_lds(t, ncol, P, s, 2, 2), false};
+  if (tps2 && fits(2, 1)) return {false, 2, false, x6_lds(t, ncol, P, s, 2), false};
+  if (db && K >= min_kst && fits(1, 2)) return {false, 1, true, x6_lds(t, ncol, P, s, 1, 2), false};
+  return {false, 1, false, x6_lds(t, ncol, P, s), false};
+}
+// ps: the phase factor of a phase-decomposed strided conv (its rows gather s phases: no 16-byte staging)
+inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d, int ps = 0) {
+  X6Variant v = x6_variant_base(t, P, K, s, d);
+  v.b4 = !v.pw && s == 1 && ps == 0 && t.WM * t.WN == 16 && x6_b4_on();
+  return v;
+}
+inline bool x6_b4_fits(const ConvArgs& a) {
+  return a.ps == 0 && a.s == 1 && a.Tin % 4 == 0 && a.xbs % 4 == 0 && ((unsigned long long)a.x & 15) == 0;
 }
 
 template <int MT, int NT, int WM, int WN, int P>
@@ -512,9 +599,21 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
                  : nullptr;
   const size_t lds = x6_lds(t, ncol, P, a.s);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
-  const X6Variant v = x6_variant(t, P, a.K, a.s, a.d);
+  const X6Variant v = x6_variant(t, P, a.K, a.s, a.d, a.ps);
   constexpr int T2 = P <= 2 ? 2 : 1;
   constexpr bool D2 = P <= 2;
+  if constexpr (WM * WN == 16) {  // 16-byte input staging: the 16-wave tile's multi-tap variant of each precision
+    if (v.b4 && x6_b4_fits(a)) {
+      constexpr int T4 = P == 1 ? 4 : P == 2 ? 2 : 1;
+      constexpr bool D4 = P == 1;  // the k7 variants: bf16 4 taps over two B buffers, h3 2 taps, x6 1
+      if (v.tps == T4 && v.db == D4) {
+        hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T4, D4, true>), dim3(a.nwg), dim3(NTHR), v.lds,
+                           st, a);
+        BC_CHECK_LAUNCH();
+        return BC_OK;
+      }
+    }
+  }
   if constexpr (P == 1 && WM * WN == 16) {
     if (v.tps == 4) {
       hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 4, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);

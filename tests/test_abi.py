@@ -256,19 +256,22 @@ def test_kernel_names_come_from_the_launchers():
             mt, nt, wm, wn = L.X6_CFGS[base % 100 + 100]
             planes = {1: 3, 2: 1, 3: 2}[base // 100]
             assert name.startswith(f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, "), (cfg, name)
-            # <..., planes, pointwise, taps per K-step, double-buffered B>
-            assert re.search(r", (true, 1, false|false, [12], (true|false))>$", name), name
+            # <..., planes, pointwise, taps per K-step, double-buffered B, 16-byte input staging>
+            assert re.search(r", (true, 1, false, false|false, [124], (true|false), (true|false))>$", name), name
         else:
             mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
             assert name == f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>", name
-    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false>")  # pointwise
-    # k7 C = 768: the 16-wave 192 x 256 tile, two taps per K-step; the final k3 keeps the double-buffered 256 x 256
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false, false>")  # pointwise
+    # k7 C = 768: the 16-wave 192 x 256 tile, two taps per K-step, 16-byte input staging; the final k3 keeps the
+    # double-buffered 256 x 256; the phase-decomposed stride-5 conv on the 16-wave tile stages single floats
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3) == \
-        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>"
-    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 3), 3).endswith("false, 1, true>")
+        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, true>"
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 3), 3).endswith("false, 1, true, false>")
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 384, 10, 5, 1, 3), 10, 5, 1) == \
+        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, false>"
     # bf16 on the 16-wave tile: four taps per K-step over the double B buffer
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(384, 384, 7, 1, 3, 2), 7, 1, 3) == \
-        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true>"
+        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true, true>"
     # C = 48 in h3: the streaming strip kernel (one per dilation); C = 96: the one-launch x6-family unit
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 1, 3), 48, 1) == "resunit_strip_kernel<1>"
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 9, 3), 48, 9) == "resunit_strip_kernel<9>"

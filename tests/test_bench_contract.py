@@ -6,9 +6,9 @@ import bench
 def test_kernel_peak_by_operand_planes():
     bf16, h3, x6 = bench.BF16_MFMA_PEAK_TFLOPS, bench.BF16_MFMA_PEAK_TFLOPS / 3, bench.BF16_MFMA_PEAK_TFLOPS / 6
     cases = {
-        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>": h3,
-        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true>": bf16,
-        "conv1d_x6_kernel<6, 1, 1, 8, 3, false, 1, false>": x6,
+        "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, true>": h3,
+        "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true, true>": bf16,
+        "conv1d_x6_kernel<6, 1, 1, 8, 3, false, 1, false, false>": x6,
         "resunit_x6_kernel<6, 1, 1, 8, 2, 2>": h3,
         "resunit_x6_kernel<6, 1, 1, 8, 1, 2>": bf16,
         "resunit_rr_kernel<96, 2, 1>": h3,

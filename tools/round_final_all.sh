@@ -13,5 +13,5 @@ for c in 3 4 5 6; do
 done
 PMC_TIMEOUT=300 bash tools/gpu_pmc.sh || { echo "pmc failed $?"; exit 1; }
 python -c "import json; d=json.loads(open('gpurun_out/final/bench_config2.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel'], r['avg_launch_ms'], r['frac'], d['parity']['vs_reference_fixture']['index_mismatches'], d['x6']['value'])"
-grep -m1 "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false>" gpurun_out/stats/run_kernel_stats.csv
+grep -m1 "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, true>" gpurun_out/stats/run_kernel_stats.csv
 echo done
