@@ -356,7 +356,7 @@ int synth_clips_launch(float* x, int B, long long T, long long clip0, hipStream_
 // One thread per 4 consecutive outputs (16-byte stores where the row allows).
 __global__ void __launch_bounds__(256) convT_interleave_kernel(const float* __restrict__ ph, const float* __restrict__ ph2,
                                                                float* __restrict__ y, float* __restrict__ y2, int Tout,
-                                                               int Q4, long long plane, ConvTInterleave il) {
+                                                               int Q4, long long plane, ConvTInterleave il, bool vec) {
   const long long row = blockIdx.y;  // b * Cout + co
   const int t0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (t0 >= Tout) return;
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(256) convT_interleave_kernel(const float* __re
   }
   float* yr = y + row * Tout;
   float* y2r = y2 ? y2 + row * Tout : nullptr;
-  if (t0 + 3 < Tout && (Tout & 3) == 0) {
+  if (vec && t0 + 3 < Tout) {  // vec: Tout % 4 == 0 and y / y2 16-byte aligned (callers may pass views)
     *reinterpret_cast<floatx4*>(yr + t0) = floatx4{v[0], v[1], v[2], v[3]};
     if (y2r) *reinterpret_cast<floatx4*>(y2r + t0) = floatx4{v2[0], v2[1], v2[2], v2[3]};
   } else {
@@ -390,11 +390,12 @@ int convT_interleave_launch(const float* ph, const float* ph2, float* y, float* 
   if (rows <= 0 || Tout <= 0) return BC_OK;
   if (rows > 65535 * 1024LL) return BC_ERR_UNSUPPORTED;
   const int gx = (Tout + 1023) / 1024;
+  const bool vec = (Tout & 3) == 0 && (((unsigned long long)y | (unsigned long long)y2) & 15) == 0;
   // grid.y is limited to 65535: fold the rows into chunks
   for (long long r0 = 0; r0 < rows; r0 += 65535) {
     const int ny = (int)(rows - r0 < 65535 ? rows - r0 : 65535);
     hipLaunchKernelGGL(convT_interleave_kernel, dim3(gx, ny), dim3(256), 0, st, ph + r0 * Q4, ph2 ? ph2 + r0 * Q4 : nullptr,
-                       y + r0 * Tout, y2 ? y2 + r0 * Tout : nullptr, Tout, Q4, (long long)rows * Q4, il);
+                       y + r0 * Tout, y2 ? y2 + r0 * Tout : nullptr, Tout, Q4, (long long)rows * Q4, il, vec);
     BC_CHECK_LAUNCH();
   }
   return BC_OK;
