@@ -63,3 +63,50 @@ def test_stream_rejects_bad_chunks_and_non_causal(dev):
     enc_nc, *_ = build_models("debug", device=dev)
     with pytest.raises(ValueError):
         StreamingEncoder(enc_nc)
+
+
+@pytest.mark.parametrize("model,B,chunks", [("base", 2, (7, 16)), ("debug", 2, (5, 12)), ("default", 1, (6, 13))])
+@pytest.mark.parametrize("sprec", ["x6", "h3"])
+def test_stream_decode_equals_whole_sequence(dev, model, B, chunks, sprec):
+    """Causal streaming DECODE (streaming.StreamingDecoder; vq/module.py:50-57 CausalConvTranspose1d carried as one
+    input frame per upsampler): the chunked stream of post-VQ latents equals the whole-sequence causal decode,
+    two chunkings bit for bit in x6, <= 1e-6 (x6) / 1e-5 (h3) of max|wav| against the whole pass; the token
+    stream (vq2emb per chunk) equals it too; the whole-sequence causal decoder is within 1e-4 of the oracle."""
+    from audiotokenization_amd.streaming import StreamingDecoder
+
+    old = L.precision_mode()
+    try:
+        L.set_precision(sprec)
+        enc, dec, esd, dsd, ek, dk = build_models(model, device=dev, causal=True)
+        n = 6000 if model != "debug" else 5760
+        x = torch.from_numpy(synth.synth_clips(B, n, clip0=23)).unsqueeze(1).to(dev)
+        s = StreamingDecoder(dec)
+        with torch.no_grad():
+            post, codes, _ = dec(enc(x), vq=True)
+            full = dec(post, vq=False)
+            a = s.decode(post, chunks[0])
+            b = s.decode(post, chunks[1])
+            tok = codes.permute(1, 2, 0).contiguous()  # (B, F, Nq): the token files' layout, batched
+            s.reset()
+            t = torch.cat([s.tokens(tok[:, i:i + chunks[0]]) for i in range(0, tok.shape[1], chunks[0])], dim=2)
+            torch.cuda.synchronize()
+        assert a.shape == full.shape == b.shape == (B, 1, n)
+        if sprec == "x6":
+            assert torch.equal(a, b), f"two chunkings differ: {max_rel_err(a, b):.3e}"
+        err = max_rel_err(a, full)
+        print(f"stream decode {model} [{sprec}] chunks {chunks}: max rel diff to the whole pass {err:.2e}, "
+              f"chunkings {max_rel_err(a, b):.2e}, tokens {max_rel_err(t, a):.2e}")
+        assert err <= (1e-6 if sprec == "x6" else 1e-5), err
+        assert max_rel_err(t, a) <= 1e-6
+        wav_ref = O.decoder_forward(post.cpu(), torch_sd(dsd), dk)
+        assert_close_rel(full.cpu(), wav_ref, 1e-4, "causal whole-sequence decode vs oracle")
+    finally:
+        L._mode = old
+
+
+def test_stream_decode_rejects_non_causal(dev):
+    from audiotokenization_amd.streaming import StreamingDecoder
+
+    _, dec, *_ = build_models("debug", device=dev)
+    with pytest.raises(ValueError):
+        StreamingDecoder(dec)
