@@ -12,7 +12,11 @@ import threading
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbigcodec_hip.so")
+# BIGCODEC_DEBUG=1: the bounds-checked debug build (build_lib.build(debug=True), _debug/; include/bigcodec.h
+# bc_debug_status) instead of the product library
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                       "_debug" if os.environ.get("BIGCODEC_DEBUG") == "1" else "")
+_LIB_PATH = os.path.join(LIB_DIR, "libbigcodec_hip.so")
 _lock = threading.Lock()
 _lib = None
 
@@ -63,9 +67,11 @@ _SIGS = {
     "bc_flac_decode": (L, [P, L, P, I, L, I]),
     "bc_conv1d_kernel_name": (I, [I, I, I, I, C.c_char_p, I]),
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
+    "bc_debug_status": (I, [P]),
+    "bc_debug_selftest": (I, [I, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 11  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 12  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -383,3 +389,17 @@ def ptr_array(ptrs):
     for i, p in enumerate(ptrs):
         arr[i] = p
     return arr
+
+
+def debug_status():
+    """(failed index checks, first failing source line) since the last call, from the bounds-checked debug
+    build (BIGCODEC_DEBUG=1; synchronises the device), or None in the product build (no checks compiled)."""
+    import torch
+
+    torch.cuda.synchronize()
+    out = (C.c_uint * 2)()
+    rc = load().bc_debug_status(C.cast(out, C.c_void_p))
+    if rc == 3:
+        return None
+    check(rc, "bc_debug_status")
+    return int(out[0]), int(out[1])

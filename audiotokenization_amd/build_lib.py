@@ -40,26 +40,38 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the BigCodec HIP library cannot be built")
 
 
-def _digest() -> str:
+DEBUG_DIR = os.path.join(PKG_DIR, "_debug")
+
+
+def _paths(debug: bool):
+    """(build dir, library, flags) of the product build or of the bounds-checked debug build (-DBC_DEBUG, in
+    _debug/ next to its own copy of the torch ops library, loaded by the package when BIGCODEC_DEBUG=1)."""
+    if debug:
+        return os.path.join(DEBUG_DIR, "_build"), os.path.join(DEBUG_DIR, "libbigcodec_hip.so"), CFLAGS + ["-DBC_DEBUG"]
+    return BUILD, LIB, CFLAGS
+
+
+def _digest(flags=None) -> str:
     h = hashlib.sha256()
     for f in SOURCES + HEADERS:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     with open(os.path.join(REPO, "include", "bigcodec.h"), "rb") as fh:
         h.update(fh.read())
-    h.update(" ".join(CFLAGS).encode())
+    h.update(" ".join(flags or CFLAGS).encode())
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile (if sources changed) and return the path of libbigcodec_hip.so."""
-    os.makedirs(BUILD, exist_ok=True)
-    stamp = os.path.join(BUILD, "stamp")
-    dig = _digest()
-    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+def build(force: bool = False, verbose: bool = False, debug: bool = False) -> str:
+    """Compile (if sources changed) and return the path of libbigcodec_hip.so (debug: the bounds-checked build)."""
+    build_dir, lib_path, flags = _paths(debug)
+    os.makedirs(build_dir, exist_ok=True)
+    stamp = os.path.join(build_dir, "stamp")
+    dig = _digest(flags)
+    if not force and os.path.exists(lib_path) and os.path.exists(stamp):
         with open(stamp) as fh:
             if fh.read().strip() == dig:
-                return LIB
+                return lib_path
     hipcc = _hipcc()
 
     common = hashlib.sha256()  # every header (any source may include any of them) + the flags
@@ -68,10 +80,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
             common.update(fh.read())
     with open(os.path.join(REPO, "include", "bigcodec.h"), "rb") as fh:
         common.update(fh.read())
-    common.update(" ".join(CFLAGS).encode())
+    common.update(" ".join(flags).encode())
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
         h = common.copy()
         with open(os.path.join(CSRC, src), "rb") as fh:
             h.update(fh.read())
@@ -80,7 +92,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             with open(ostamp) as fh:
                 if fh.read().strip() == h.hexdigest():
                     return obj  # unchanged source and headers: keep the object
-        cmd = [hipcc, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         res = subprocess.run(cmd, capture_output=True, text=True)
@@ -92,18 +104,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8, 16)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-soname,libbigcodec_hip.so", *objs, "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib_path)
     with open(stamp, "w") as fh:
         fh.write(dig)
-    return LIB
+    return lib_path
 
 
-def _ops_flags():
+def _ops_flags(debug: bool = False):
     import torch
     import torch.utils.cpp_extension as ce
 
@@ -112,39 +124,42 @@ def _ops_flags():
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     return (["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=bigcodec_ops"] + inc,
-            libs + ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", f"-L{PKG_DIR}", "-lbigcodec_hip",
+            libs + ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", f"-L{DEBUG_DIR if debug else PKG_DIR}", "-lbigcodec_hip",
                     "-Wl,-rpath,$ORIGIN"], torch.__version__)
 
 
-def build_ops(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/torch_ops.cpp (if it, the header or torch changed) into libbigcodec_ops.so."""
-    build(verbose=verbose)
-    cflags, ldflags, tv = _ops_flags()
+def build_ops(force: bool = False, verbose: bool = False, debug: bool = False) -> str:
+    """Compile csrc/torch_ops.cpp (if it, the header or torch changed) into libbigcodec_ops.so (debug: the copy in
+    _debug/ that links the bounds-checked libbigcodec_hip.so next to it)."""
+    build(verbose=verbose, debug=debug)
+    cflags, ldflags, tv = _ops_flags(debug)
     h = hashlib.sha256()
     for f in (os.path.join(CSRC, OPS_SRC), os.path.join(REPO, "include", "bigcodec.h")):
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update((" ".join(cflags + ldflags) + tv).encode())
     dig = h.hexdigest()
-    stamp = os.path.join(BUILD, "ops_stamp")
-    if not force and os.path.exists(OPS_LIB) and os.path.exists(stamp):
+    ops_lib = os.path.join(DEBUG_DIR, "libbigcodec_ops.so") if debug else OPS_LIB
+    stamp = os.path.join(_paths(debug)[0], "ops_stamp")
+    if not force and os.path.exists(ops_lib) and os.path.exists(stamp):
         with open(stamp) as fh:
             if fh.read().strip() == dig:
-                return OPS_LIB
+                return ops_lib
     cxx = os.environ.get("CXX", "g++")
-    tmp = OPS_LIB + ".tmp"
+    tmp = ops_lib + ".tmp"
     cmd = [cxx, *cflags, os.path.join(CSRC, OPS_SRC), "-o", tmp, *ldflags]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"{cxx} failed for {OPS_SRC}:\n{res.stderr}")
-    os.replace(tmp, OPS_LIB)
+    os.replace(tmp, ops_lib)
     with open(stamp, "w") as fh:
         fh.write(dig)
-    return OPS_LIB
+    return ops_lib
 
 
-if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
-    print(build_ops(force="--force" in sys.argv, verbose=True))
+if __name__ == "__main__":  # python audiotokenization_amd/build_lib.py [--force] [--debug]
+    dbg = "--debug" in sys.argv
+    print(build(force="--force" in sys.argv, verbose=True, debug=dbg))
+    print(build_ops(force="--force" in sys.argv, verbose=True, debug=dbg))

@@ -333,7 +333,7 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   ConvArgs a{};
   a.x = lin; a.w = wih; a.bias = bias; a.res = nullptr;
   a.osa = nullptr; a.osb = nullptr; a.y = gx; a.y2 = nullptr;
-  a.xbs = 0; a.ybs = 0; a.rbs = 0;
+  a.xbs = Cin * tb; a.ybs = 4LL * H * tb; a.rbs = 0;  // one "batch item" (B = 1): the extents (debug-build checks)
   a.Cin = Cin; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
   a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
   a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
@@ -551,3 +551,52 @@ extern "C" int bc_debug_set_lstm_presplit(int on) {
   g_lstm_presplit = on ? 1 : 0;
   return old;
 }
+
+// ---- bounds-checked debug build (include/bigcodec.h) -------------------------------------------------------------
+#ifdef BC_DEBUG
+namespace bc {
+__global__ void debug_selftest_kernel(int n) {
+  if (!BC_DOK((int)(blockIdx.x * blockDim.x + threadIdx.x) >= n)) return;  // lanes < n fail on purpose
+}
+}  // namespace bc
+BC_DEBUG_EXPORT(abi)
+extern "C" {
+int bc_dbg_fetch_conv1d(unsigned*);
+int bc_dbg_fetch_conv1d_x6_p1(unsigned*);
+int bc_dbg_fetch_conv1d_x6_p2(unsigned*);
+int bc_dbg_fetch_conv1d_x6_p3(unsigned*);
+int bc_dbg_fetch_resunit_x6(unsigned*);
+int bc_dbg_fetch_resunit_rr(unsigned*);
+int bc_dbg_fetch_pw_presplit(unsigned*);
+int bc_dbg_fetch_lstm_seq(unsigned*);
+int bc_debug_status(unsigned* out) {
+  if (!out) return BC_ERR_ARG;
+  if (hipDeviceSynchronize() != hipSuccess) return BC_ERR_LAUNCH;
+  out[0] = out[1] = 0;
+  int (*const fetch[])(unsigned*) = {bc_dbg_fetch_conv1d, bc_dbg_fetch_conv1d_x6_p1, bc_dbg_fetch_conv1d_x6_p2,
+                                     bc_dbg_fetch_conv1d_x6_p3, bc_dbg_fetch_resunit_x6, bc_dbg_fetch_resunit_rr,
+                                     bc_dbg_fetch_pw_presplit, bc_dbg_fetch_lstm_seq, bc_dbg_fetch_abi};
+  for (auto f : fetch)
+    if (f(out)) return BC_ERR_LAUNCH;
+  return BC_OK;
+}
+int bc_debug_selftest(int n, void* stream) {
+  if (n < 0 || n > 1 << 20) return BC_ERR_ARG;
+  if (n == 0) return BC_OK;
+  hipLaunchKernelGGL(debug_selftest_kernel, dim3((n + 255) / 256 + 1), dim3(256), 0, S(stream), n);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+}
+#else
+extern "C" {
+int bc_debug_status(unsigned* out) {
+  if (out) out[0] = out[1] = 0;
+  return BC_ERR_UNSUPPORTED;
+}
+int bc_debug_selftest(int n, void* stream) {
+  (void)n, (void)stream;
+  return BC_ERR_UNSUPPORTED;
+}
+}
+#endif

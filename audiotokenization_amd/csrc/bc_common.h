@@ -28,6 +28,38 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #define BC_ABL(flags, bit) 0
 #endif
 
+// Bounds-checked debug build: `-DBC_DEBUG` (build_lib.build(debug=True) ->
+// libbigcodec_hip_debug.so, loaded when BIGCODEC_DEBUG=1).  BC_DOK(cond) guards a global access whose index a
+// kernel computed (epilogue stores and residual reads, weight copies, the LSTM's hand-off slots): a failed check
+// counts into this translation unit's bc_dbg_word (failures, first failing source line) with vector atomics and
+// the access is SKIPPED, so the kernel cannot fault; bc_debug_status() (abi.hip) reads and clears every unit's
+// words.  In the product library BC_DOK is the constant true and the guards vanish.
+#ifdef BC_DEBUG
+namespace bc {
+static __device__ unsigned bc_dbg_word[2];
+__device__ __noinline__ static bool bc_dbg_fail(unsigned line) {
+  atomicAdd(&bc_dbg_word[0], 1u);
+  atomicCAS(&bc_dbg_word[1], 0u, line);
+  return false;
+}
+}  // namespace bc
+#define BC_DOK(cond) ((cond) ? true : ::bc::bc_dbg_fail(__LINE__))
+// host reader of this translation unit's words (read and cleared; out[0] failures, out[1] first line)
+#define BC_DEBUG_EXPORT(tu)                                                                       \
+  extern "C" int bc_dbg_fetch_##tu(unsigned* out) {                                               \
+    unsigned w[2] = {0, 0};                                                                       \
+    if (hipMemcpyFromSymbol(w, HIP_SYMBOL(::bc::bc_dbg_word), sizeof(w)) != hipSuccess) return 2; \
+    const unsigned z[2] = {0, 0};                                                                 \
+    if (hipMemcpyToSymbol(HIP_SYMBOL(::bc::bc_dbg_word), z, sizeof(z)) != hipSuccess) return 2;   \
+    out[0] += w[0];                                                                               \
+    if (!out[1]) out[1] = w[1];                                                                   \
+    return 0;                                                                                     \
+  }
+#else
+#define BC_DOK(cond) true
+#define BC_DEBUG_EXPORT(tu)
+#endif
+
 namespace bc {
 
 // sin(x) for the Snake: Cody-Waite reduction by pi in 4 fma steps (valid for |x| < 39000), odd

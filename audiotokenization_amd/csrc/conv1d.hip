@@ -322,3 +322,5 @@ int conv_launch(ConvArgs& a, int B, int cfg_id, hipStream_t st) {
 #undef BC_TILE_CASES
 
 }  // namespace bc
+
+BC_DEBUG_EXPORT(conv1d)

@@ -113,6 +113,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     const int n = (K - t0 < TPS ? K - t0 : TPS) * a_pieces;
     const unsigned char* src = wblk + (long long)(c * K + t0) * (a_pieces * 1024);
     unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
+    // debug build: the copy stays inside this m-group's packed weights
+    if (!BC_DOK(mt_idx < a.ntm && c < a.nchunks && t0 * a_pieces + n <= K * a_pieces)) return;
     for (int q = wave; q < n; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);

@@ -8,3 +8,5 @@ int x6_launch_tile<1>(ConvArgs& a, int B, int tile, hipStream_t st) {
   BC_X6_TILE_SWITCH(1)
 }
 }  // namespace bc
+
+BC_DEBUG_EXPORT(conv1d_x6_p1)

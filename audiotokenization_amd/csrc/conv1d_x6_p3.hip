@@ -8,3 +8,5 @@ int x6_launch_tile<3>(ConvArgs& a, int B, int tile, hipStream_t st) {
   BC_X6_TILE_SWITCH(3)
 }
 }  // namespace bc
+
+BC_DEBUG_EXPORT(conv1d_x6_p3)

@@ -314,7 +314,10 @@ __global__ void __launch_bounds__(256, 1) lstm_seq_x6_kernel(LstmSeqArgs a) {
     // layer output (read only after the launch): off the publishing wave's critical path
 #pragma unroll
     for (int q = 0; q < 2; ++q)
-      if (cb[q] < a.nb) a.y[(long long)(g * LS_U + cu[q]) * TB + (long long)t * a.Btot + a.b0 + cb[q]] = hq[q];
+      if (cb[q] < a.nb) {
+        const long long yi = (long long)(g * LS_U + cu[q]) * TB + (long long)t * a.Btot + a.b0 + cb[q];
+        if (BC_DOK(yi < (long long)H * TB)) a.y[yi] = hq[q];
+      }
     // next step's input-projection gates: issued after this step's publish drain so that drain does
     // not wait for them; they land during the next step's poll and MFMAs
     if (t + 1 < a.T) {
@@ -577,7 +580,10 @@ __global__ void __launch_bounds__(256, 1) lstm_seq2_x6_kernel(LstmSeqArgs a) {
         pend_v = (unsigned)(t + 1 + sh);
       }
       LS2_STAMP(6)
-      if (ok) a.y[(long long)(g * LS_U + cu) * TB + (long long)t * a.Btot + a.b0 + clip] = hq;
+      if (ok) {
+        const long long yi = (long long)(g * LS_U + cu) * TB + (long long)t * a.Btot + a.b0 + clip;
+        if (BC_DOK(yi < (long long)a.H * TB)) a.y[yi] = hq;
+      }
       if (t + 1 == a.T && ok) {  // carried state out
         if (a.hT) a.hT[unit_row + clip] = hq;
         if (a.cT) a.cT[unit_row + clip] = c;
@@ -837,3 +843,5 @@ extern "C" int bc_debug_lstm_stamps(long long* host, long long n) {
   if (!p || !host || n <= 0 || n > 2LL * bc::LS_STAMP_T * 32) return 1;
   return hipMemcpy(host, p, sizeof(long long) * n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
 }
+
+BC_DEBUG_EXPORT(lstm_seq)

@@ -246,3 +246,5 @@ int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st) {
 }
 
 }  // namespace bc
+
+BC_DEBUG_EXPORT(pw_presplit)

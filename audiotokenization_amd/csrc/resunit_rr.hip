@@ -908,3 +908,5 @@ int resunit_rr_launch(const float* x_raw, const float* x_act, const float* w7, c
 }
 
 }  // namespace bc
+
+BC_DEBUG_EXPORT(resunit_rr)

@@ -108,6 +108,7 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
     const int n = (K - t0 < TPS ? K - t0 : TPS) * a_pieces;
     const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)(c * K + t0) * (a_pieces * 1024);
     unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
+    if (!BC_DOK(c < a.nchunks && t0 * a_pieces + n <= K * a_pieces)) return;  // debug build: inside the packed k7 weights
     for (int q = wave; q < n; q += 8)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
   for (int kc = 0; kc < KC1; ++kc)
 #pragma unroll
     for (int p = 0; p < P; ++p)
-      w1f[kc][p] = (p2 && kc < r.nck1)
+      w1f[kc][p] = (p2 && kc < r.nck1 && BC_DOK(mq < QA))
                        ? *reinterpret_cast<const frag_t*>(reinterpret_cast<const unsigned char*>(r.w1) +
                                                           ((kc * P + p) * QA + mq) * 1024 + lane * 16)
                        : frag_t{};
@@ -626,3 +627,5 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
 }
 
 }  // namespace bc
+
+BC_DEBUG_EXPORT(resunit_x6)

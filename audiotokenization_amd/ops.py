@@ -19,7 +19,7 @@ import torch
 
 from . import _lib as L
 
-OPS_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbigcodec_ops.so")
+OPS_PATH = os.path.join(L.LIB_DIR, "libbigcodec_ops.so")  # next to the libbigcodec_hip.so it links ($ORIGIN)
 _lock = threading.Lock()
 _ns = None
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 11
+#define BC_ABI_VERSION 12
 
 int bc_abi_version(void);
 
@@ -281,6 +281,18 @@ int bc_btc_to_ctb(const float* x, float* y, int B, int C, int T, void* stream);
 int bc_ctb_to_btc_add(const float* y, const float* skip, float* out, int B, int C, int T,
                       void* stream);
 int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream);
+
+/* ---- Bounds-checked debug build (no reference counterpart: SURVEY.md §5 row 2) ------------------------------
+ * libbigcodec_hip.so built with -DBC_DEBUG (build_lib.build(debug=True) -> audiotokenization_amd/_debug/, loaded by
+ * the Python package when BIGCODEC_DEBUG=1) checks the indices of the kernels' computed global accesses (conv /
+ * ResidualUnit epilogue stores and residual reads, weight copies, ResLSTM output stores); a failed check is counted
+ * and its access skipped, so a bad launch reports instead of faulting the GPU.
+ * bc_debug_status(out[2]): out[0] = failed checks since the last call, out[1] = the first failing source line
+ *   (0 = none); reads and clears; synchronises the device.  Returns 3 (unsupported) in the product build.
+ * bc_debug_selftest(n, stream): a kernel whose n lanes fail one check each on purpose, touching no memory
+ *   outside the debug words (the mechanism's own test).  Returns 3 in the product build. */
+int bc_debug_status(unsigned int* out);
+int bc_debug_selftest(int n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -283,3 +283,14 @@ def test_kernel_names_come_from_the_launchers():
         assert nb.startswith("resunit_x6_kernel<") and re.search(r", 1, [124]>$", nb), nb
     with pytest.raises(L.BigCodecLibraryError):
         L.conv_kernel_name(12345, 7)
+
+
+def test_product_build_has_no_debug_checks():
+    """bc_debug_status / bc_debug_selftest exist in every build; the product library answers 3 (unsupported):
+    its index guards are compiled out (bc_common.h BC_DOK)."""
+    import ctypes
+
+    lib = L.load()
+    out = (ctypes.c_uint * 2)(7, 7)
+    assert lib.bc_debug_status(ctypes.cast(out, ctypes.c_void_p)) == 3 and list(out) == [0, 0]
+    assert lib.bc_debug_selftest(1, None) == 3
