@@ -89,15 +89,17 @@ def test_stream_decode_equals_whole_sequence(dev, model, B, chunks, sprec):
             tok = codes.permute(1, 2, 0).contiguous()  # (B, F, Nq): the token files' layout, batched
             s.reset()
             t = torch.cat([s.tokens(tok[:, i:i + chunks[0]]) for i in range(0, tok.shape[1], chunks[0])], dim=2)
+            # (the VQ forward's post embedding is straight-through, z_e + (z_q - z_e): the token path decodes z_q)
+            full_tok = dec(dec.quantizer.vq2emb_ct(tok), vq=False)
             torch.cuda.synchronize()
         assert a.shape == full.shape == b.shape == (B, 1, n)
         if sprec == "x6":
             assert torch.equal(a, b), f"two chunkings differ: {max_rel_err(a, b):.3e}"
         err = max_rel_err(a, full)
         print(f"stream decode {model} [{sprec}] chunks {chunks}: max rel diff to the whole pass {err:.2e}, "
-              f"chunkings {max_rel_err(a, b):.2e}, tokens {max_rel_err(t, a):.2e}")
+              f"chunkings {max_rel_err(a, b):.2e}, token stream vs whole token decode {max_rel_err(t, full_tok):.2e}")
         assert err <= (1e-6 if sprec == "x6" else 1e-5), err
-        assert max_rel_err(t, a) <= 1e-6
+        assert max_rel_err(t, full_tok) <= (1e-6 if sprec == "x6" else 1e-5)
         wav_ref = O.decoder_forward(post.cpu(), torch_sd(dsd), dk)
         assert_close_rel(full.cpu(), wav_ref, 1e-4, "causal whole-sequence decode vs oracle")
     finally:
