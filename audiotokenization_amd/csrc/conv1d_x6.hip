@@ -174,8 +174,43 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   return -1;
 }
 
+// Measured x6 (three-plane) preferences of round 4 (tools/x6_table_sweep.sh, profiles/r04c_x6_sweep.txt, B = 64 x 10 s
+// encoder shapes), where the round-1 table above loses: the 16-wave 192 x 256 tile (x6 without the A-fragment prefetch,
+// 16-byte input staging on stride-1 launches) on every Cout % 192 == 0 conv -- k7 C = 192 / 384 / 768 10.18 / 19.55 /
+// 13.83 -> 8.95 / 16.34 / 12.79 ms, pointwise C = 192 / 384 / 768 3.79 / 4.95 / 3.47 -> 3.31 / 4.67 / 3.19, the LSTM
+// input projection 8.99 -> 7.89, phase-decomposed stride 2 96 -> 192 / 192 -> 384 4.86 / 8.05 -> 3.97 / 6.44, stride 5
+// 768 -> 1536 10.79 -> 8.96 -- except the stride-5 384 -> 768 (phase-decomposed 256 x 256: 13.58 -> 10.94) and the final
+// k3 1536 -> 1024 (256 x 256: 4.02 -> 3.59); 48 -> 96 stride 2 keeps the 96-row tile (2109: 3.16 vs 4.89).
+static int x6p3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
+  (void)Cin;
+  auto fits = [&](int tile, int K_, int s_, int d_) { return x6_ncol(kX6Tiles[tile], K_, s_, d_) <= 32 * X6_MAXCOL_ITERS; };
+  if (s == 1 && Cout % 192 == 0 && fits(22, K, 1, d)) return 122;
+  if (s == 1 && K > 1 && Cout % 256 == 0 && fits(21, K, 1, d)) return 121;
+  const int Kp = (K + s - 1) / s;
+  if (s == 2 && d == 1 && Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 2000 + 122;
+  if (s >= 3 && s <= 16 && d == 1) {
+    if (Cout % 192 == 0 && Cout >= 1536 && fits(22, Kp, 1, 1)) return 1000 * s + 122;
+    if (Cout % 256 == 0 && fits(21, Kp, 1, 1)) return 1000 * s + 121;
+    if (Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 1000 * s + 122;
+  }
+  return -1;
+}
+
+// BC_X6_TABLE=1 restores the round-1 x6 table (A/B timing).
+static bool x6_table_r4() {
+  static const bool v = [] {
+    const char* e = getenv("BC_X6_TABLE");
+    return !e || atoi(e) != 1;
+  }();
+  return v;
+}
+
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   if (Cin < 16) return -1;  // e.g. the first conv (Cin = 1): no K to amortise the split over
+  if (planes == 3 && x6_occ_pref() == 0 && x6_table_r4()) {
+    const int c = x6p3_preferred_cfg(Cout, Cin, K, s, d);
+    if (c >= 0) return c;
+  }
   if (planes <= 2 && x6_occ_pref() == 0) {  // bf16 (1 plane) follows the h3 table (measured, config 5)
     const int c = h3_preferred_cfg(Cout, Cin, K, s, d);
     if (c >= 0) return c + (planes == 2 ? 200 : 100);  // (a phase-decomposed 1000 * s + tile keeps its phase factor)

@@ -25,11 +25,11 @@ from helpers import GAP_TOL, build_models, index_mismatches, max_rel_err
 
 pytestmark = pytest.mark.gpu
 
-# bf16 bounds (SURVEY §8(d) expects "a few %" index mismatches for bf16 products; the measured values are
-# printed and recorded in DESIGN.md §4): twice the measured worst case, rounded up.
+# bf16 bounds (SURVEY §8(d) expects "a few %" index mismatches for bf16 products; measured on the MI355X,
+# profiles/r04c_gpu_tests.txt: 3.11 % vs the reference, 2.89 % vs x6, latent tail 1.28e-2): about twice the measured.
 BF16_VS_REF_MAX = 0.06
 BF16_VS_FP32_MAX = 0.06
-BF16_LATENT_TOL = 5e-2
+BF16_LATENT_TOL = 3e-2
 
 
 @pytest.fixture(scope="module")
