@@ -53,20 +53,35 @@ __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ 
 constexpr int ru_min_waves(int MT, int NT, int WM, int P) {
   return (NT == 1 || (MT == 3 && NT == 2 && WM == 2)) ? 4 : 2;
 }
+// 16-wave tiles (1024 threads, one workgroup per CU, four waves per SIMD: <= 128 VGPRs) declare 1, as the conv kernel
+constexpr int ru_launch_waves(int MT, int NT, int WM, int WN, int P) {
+  return WM * WN == 16 ? 1 : ru_min_waves(MT, NT, WM, P);
+}
+// phase 2 (k=1 conv): QA m-tiles x NTT n-tiles over the NW waves, NPW n-tile groups per m-tile (the largest divisor of
+// NTT within NW / QA)
+constexpr int ru_npw(int NW, int QA, int NTT) {
+  int n = NW / QA < NTT ? NW / QA : NTT;
+  while (n > 1 && NTT % n) --n;
+  return n;
+}
 
 // TPS: k=7 taps per phase-1 K-step (one A copy, one wait and one barrier per TPS taps).
 template <int MT, int NT, int WM, int WN, int P, int TPS = 1>
-__global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
+__global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, P)) resunit_x6_kernel(ConvArgs a, ConvArgs e, RUExtra r) {
   static_assert(P >= 1 && P <= 3, "bf16, h3 or x6 operands");
   typedef typename FragType<P>::type frag_t;
-  __shared__ unsigned smax[2][8];  // P == 2: per-wave block maxima (k=7 input chunks by parity; h tile)
+  constexpr int NW = WM * WN;  // 8 waves (512 threads, two workgroups per CU) or 16 (1024, one per CU)
+  static_assert(NW == 8 || NW == 16, "512- or 1024-thread workgroups");
+  constexpr int NTHR = 64 * NW;
+  constexpr int NCG = NW / 8;  // B staging column groups (16 channel pairs x 32 column lanes each)
+  __shared__ unsigned smax[2][NW];  // P == 2: per-wave block maxima (k=7 input chunks by parity; h tile)
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;
-  constexpr int CI = (BN + 6 * RU_MAX_DIL + 31) / 32;  // 32-column B passes: ncol <= BN + 6 * d
-  // phase 2 (k=1 conv): QA m-tiles x NTT n-tiles over the 8 waves, NPW n-tile groups per m-tile
+  constexpr int CI = ((BN + 6 * RU_MAX_DIL + 31) / 32 + NCG - 1) / NCG;  // 32-column B passes per thread
+  // phase 2 (k=1 conv): QA m-tiles x NTT n-tiles over the NW waves, NPW n-tile groups per m-tile
   constexpr int NTT = NT * WN;
-  static_assert(QA <= 8, "one m-tile per wave in phase 2");
-  constexpr int NPW = (8 / QA < NTT) ? 8 / QA : NTT;
+  static_assert(QA <= NW, "one m-tile per wave in phase 2");
+  constexpr int NPW = ru_npw(NW, QA, NTT);
   constexpr int NTW = NTT / NPW;
   static_assert(NTT % NPW == 0, "n-tile groups");
   constexpr int KC1 = (16 * QA + X6_BKC - 1) / X6_BKC;  // k=1 input chunks (C = 16 * QA)
@@ -109,19 +124,21 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
     const unsigned char* src = reinterpret_cast<const unsigned char*>(w) + (long long)(c * K + t0) * (a_pieces * 1024);
     unsigned char* dst = As + buf * (TPS * a_pieces * 1024);
     if (!BC_DOK(c < a.nchunks && t0 * a_pieces + n <= K * a_pieces)) return;  // debug build: inside the packed k7 weights
-    for (int q = wave; q < n; q += 8)
+    for (int q = wave; q < n; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16), (lds_void_t)(dst + q * 1024),
                                        16, 0, 0);
   };
 
-  const int bp = tid >> 5;
+  const int bp = (tid >> 5) & 15;
   const int bcl = tid & 31;
+  const int bcg = tid >> 9;  // 0 with 8 waves
+  auto bcol = [&](int i) { return bcl + 32 * (i * NCG + bcg); };
   float bv0[CI], bv1[CI];
   auto load_b = [&](int chunk) {
     const int ci0 = chunk * X6_BKC + 2 * bp;
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
+      const int col = bcol(i);
       const int ti = in0 + col;
       const bool tin = col < ncol && ti >= 0 && ti < a.Tin;
       const unsigned o0 = (tin && ci0 < a.Cin) ? (unsigned)((ci0 * a.Tin + ti) * 4) : 0xfffffff0u;
@@ -144,7 +161,7 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
   auto bmax_scale = [&](int par) {
     unsigned m = smax[par][0];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) m = m > smax[par][w] ? m : smax[par][w];
+    for (int w = 1; w < NW; ++w) m = m > smax[par][w] ? m : smax[par][w];
     return h3_scale_from_bits(__builtin_amdgcn_readfirstlane(m));
   };
   float xs = 1.f;  // P == 2: scale of the staged k=7 input chunk and of the phase-1 accumulator
@@ -165,7 +182,7 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
   auto store_b = [&]() {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
-      const int col = bcl + 32 * i;
+      const int col = bcol(i);
       if (col < ncol) {
         if constexpr (P == 2) {
           unsigned h, m;
@@ -314,7 +331,7 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
   const int C = a.Cout;
   if (C < r.nck1 * X6_BKC) {  // zero the pad channels of the last chunk (never written below)
     const int g0 = (C % X6_BKC) / 8;
-    for (int idx = tid; idx < P * BN * 4; idx += 512) {
+    for (int idx = tid; idx < P * BN * 4; idx += NTHR) {
       const int p = idx / (BN * 4), n = (idx / 4) % BN, g = idx % 4;
       if (g >= g0)
         *reinterpret_cast<floatx4*>(Hs + p * r.hplane + (r.nck1 - 1) * (BN * 64) + hs_off(n, g)) =
@@ -462,9 +479,19 @@ __global__ void __launch_bounds__(512, ru_min_waves(MT, NT, WM, P)) resunit_x6_k
 // fragment reads per K32 unit, bit-identical outputs): 4-6 % per unit (profiles/r03m_ru_tiles.txt); x6 is
 // neutral there (7.05 vs 7.08 ms) and keeps 109.  The 48-row bf16 tiles with more columns per wave (106, 124)
 // need more than 128 VGPRs (one workgroup per CU) and run 1.8-2.1x slower than 111.
-static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 123, 124};
-static const int kRUCandidatesP12[] = {123, 109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 124};
+static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 123, 124, 125, 126};
+static const int kRUCandidatesP12[] = {123, 109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 124, 125, 126};
 constexpr size_t RU_LDS_MAX = 80 * 1024;
+// LDS budget of a candidate: two workgroups per CU for the 8-wave tiles, the whole CU for the 16-wave ones
+static size_t ru_lds_budget(const X6Tile& t) { return t.WM * t.WN == 16 ? 160 * 1024 : RU_LDS_MAX; }
+// BC_RU_W16=1 prefers the 16-wave tiles 125 / 126 (one 1024-thread workgroup per CU; A/B timing)
+static bool ru_w16() {
+  static const bool v = [] {
+    const char* e = getenv("BC_RU_W16");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
 // BC_RU_CFG forces one candidate tile (timing experiments; it must fit the 160 KiB of a CU).
 static int ru_forced_cfg() {
   static const int v = [] {
@@ -495,7 +522,7 @@ static int ru_tps(const X6Tile& t, int C, int d, int P) {
   if (forced == 1 || forced == 2 || forced == 4) return forced;
   int bp, hp;
   for (int tps : {4, 2})
-    if ((tps < 4 || C <= 64) && ru_lds(t, C, d, P, &bp, &hp, tps) <= RU_LDS_MAX) return tps;
+    if ((tps < 4 || C <= 64) && ru_lds(t, C, d, P, &bp, &hp, tps) <= ru_lds_budget(t)) return tps;
   return 1;
 }
 
@@ -504,15 +531,17 @@ int resunit_select_cfg(int C, int d, int mode) {
   if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
-  for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
-    const X6Tile& t = x6_tile(cfg);
-    if (x6_BM(t) != C) continue;
-    if (d > RU_MAX_DIL) return -1;
-    int bp, hp;
-    const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
-    if (forced ? (cfg != forced || lds > 160 * 1024) : lds > RU_LDS_MAX) continue;
-    return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
-  }
+  for (int pass = ru_w16() ? 0 : 1; pass < 2; ++pass)
+    for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
+      const X6Tile& t = x6_tile(cfg);
+      if (x6_BM(t) != C) continue;
+      if (pass == 0 && t.WM * t.WN != 16) continue;  // BC_RU_W16: the 16-wave tiles first
+      if (d > RU_MAX_DIL) return -1;
+      int bp, hp;
+      const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
+      if (forced ? (cfg != forced || lds > 160 * 1024) : lds > ru_lds_budget(t)) continue;
+      return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
+    }
   return -1;
 }
 
@@ -534,7 +563,7 @@ bool resunit_cfg_ok(int cfg, int C, int d) {
 
 template <int MT, int NT, int WM, int WN, int P>
 static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st) {
-  constexpr int BN = 16 * NT * WN;
+  constexpr int BN = 16 * NT * WN, NTHR = 64 * WM * WN;
   const X6Tile t{MT, NT, WM, WN};
   int bplane, hplane;
   const int tps = ru_tps(t, a.Cout, a.d, P);
@@ -560,11 +589,11 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
                                            (long long)r.nck1 * P * QA * 1024);
   }
   if (P != 3 && tps == 4)
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 4 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 4 : 1)>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
   else if (P != 3 && tps == 2)
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 2 : 1)>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 2 : 1)>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
   else
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(512), lds, st, a, e, r);
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }
@@ -572,7 +601,7 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
   if (mode < 1 || mode > 3 || !resunit_cfg_ok(cfg, C, d)) return -1;
-  if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
+  if (mode == 3 && cfg != 326 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, P,
@@ -583,7 +612,8 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
                    const float* isa, const float* isb) {
-  if (cfg >= 300 && cfg < 400 && resunit_rr_ok(C, d)) {  // h3 at C = 48 / 96: the register-weight kernel
+  // h3 at C = 48: the register-weight / strip kernels (not when a 16-wave one-launch tile is asked for, A/B timing)
+  if (cfg >= 300 && cfg < 400 && cfg != 326 && resunit_rr_ok(C, d)) {
     const int rc = resunit_rr_launch(x_raw, x_act, w7, b7, s2a, s2b, w1, b1, osa, osb, y, y2, B, C, T, d, pl, st,
                                      isa, isb);
     if (rc != BC_ERR_UNSUPPORTED) return rc;
@@ -621,6 +651,8 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
     BC_RU_CASES(17, 4, 1, 2, 4)
     BC_RU_CASES(23, 3, 2, 2, 4)
     BC_RU_CASES(24, 3, 4, 1, 8)
+    BC_RU_CASES(25, 3, 2, 2, 8)
+    BC_RU_CASES(26, 3, 2, 1, 16)
   }
 #undef BC_RU_CASES
   return BC_ERR_ARG;

@@ -24,4 +24,15 @@ r = d["roofline"]; x = d["x6"]; rr = x["roofline"]
 print(d["value"], d["ms_per_step"], r["kernel"], r["avg_launch_ms"], r["frac"])
 print("x6", x["value"], x["ms_per_step"], rr["kernel"], rr["avg_launch_ms"], rr["frac"], x["parity"]["index_mismatches"])
 PY
+
+# one-launch ResidualUnit: 8-wave 96 x 128 (323) vs 16-wave 96 x 256 (325) at C = 96, strip vs 16-wave 48 x 512 (326)
+# at C = 48, h3, snake on load (as the encoder runs them), encoder shapes
+for d in 1 3 9; do
+  for c in 323 325; do timeout -k 10 120 python tools/ru_bench.py --C 96 --d $d --T 120000 --lazy --cfg $c >> $O/ru_ab.txt 2>&1 || exit 1; done
+  for c in 311 326; do timeout -k 10 120 python tools/ru_bench.py --C 48 --d $d --T 240000 --lazy --cfg $c >> $O/ru_ab.txt 2>&1 || exit 1; done
+done
+for d in 1 9; do
+  for c in 323 325; do BC_RU_TPS=4 timeout -k 10 120 python tools/ru_bench.py --C 96 --d $d --T 120000 --lazy --cfg $c >> $O/ru_ab.txt 2>&1 || exit 1; done
+done
+grep resunit $O/ru_ab.txt
 echo done
