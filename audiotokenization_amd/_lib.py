@@ -323,8 +323,7 @@ X6_CFGS = {100 + i: t for i, t in enumerate([(4, 4, 2, 4), (4, 2, 2, 4), (4, 2, 
                                               (6, 2, 2, 4), (6, 1, 2, 4), (3, 1, 2, 4), (4, 1, 2, 4),
                                               (8, 2, 2, 4), (4, 4, 4, 2), (6, 4, 2, 4), (8, 4, 2, 4),
                                               (6, 2, 2, 8),  # 122: 16 waves (h3, bf16 and x6)
-                                              (3, 2, 2, 4), (3, 4, 1, 8),  # 123, 124: one-launch ResidualUnit only
-                                              (3, 2, 2, 8), (3, 2, 1, 16)])}  # 125, 126: the same, 16 waves
+                                              (3, 2, 2, 4), (3, 4, 1, 8)])}  # 123, 124: one-launch ResidualUnit only
 
 
 _name_cache = {}

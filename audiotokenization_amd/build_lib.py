@@ -51,6 +51,11 @@ def _paths(debug: bool):
     return BUILD, LIB, CFLAGS
 
 
+def stamp_path(debug: bool = False) -> str:
+    """The built library's source digest (the debug one next to its library: _debug/_build stays off the GPU box)."""
+    return os.path.join(DEBUG_DIR, "stamp") if debug else os.path.join(BUILD, "stamp")
+
+
 def _digest(flags=None) -> str:
     h = hashlib.sha256()
     for f in SOURCES + HEADERS:
@@ -66,7 +71,7 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False) -> st
     """Compile (if sources changed) and return the path of libbigcodec_hip.so (debug: the bounds-checked build)."""
     build_dir, lib_path, flags = _paths(debug)
     os.makedirs(build_dir, exist_ok=True)
-    stamp = os.path.join(build_dir, "stamp")
+    stamp = stamp_path(debug)
     dig = _digest(flags)
     if not force and os.path.exists(lib_path) and os.path.exists(stamp):
         with open(stamp) as fh:

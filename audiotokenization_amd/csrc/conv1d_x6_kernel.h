@@ -485,8 +485,6 @@ inline constexpr X6Tile kX6Tiles[] = {
     // one-launch ResidualUnit only (resunit_x6.hip; the conv kernel does not instantiate them):
     {3, 2, 2, 4},  // 123: BM=96  BN=128, 48 x 32 per wave (C = 96: 10 instead of 14 LDS fragment reads per K32)
     {3, 4, 1, 8},  // 124: BM=48  BN=512, 48 x 64 per wave (bf16 C = 48: 7 reads per 12 MFMAs instead of 4 per 3)
-    {3, 2, 2, 8},  // 125: BM=96  BN=256, 16 waves of 48 x 32 (C = 96, one 1024-thread workgroup per CU)
-    {3, 2, 1, 16}, // 126: BM=48  BN=512, 16 waves of 48 x 32 (C = 48)
 };
 constexpr int X6_NT = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -677,9 +675,7 @@ int x6_launch_tile(ConvArgs& a, int B, int tile, hipStream_t st);
     case 21: return launch_x6<8, 4, 2, 4, P>(a, B, st);            \
     case 22: return launch_x6_w16<P>(a, B, st);                    \
     case 23:                                                       \
-    case 24:                                                       \
-    case 25:                                                       \
-    case 26: return BC_ERR_UNSUPPORTED;                            \
+    case 24: return BC_ERR_UNSUPPORTED;                            \
   }                                                                \
   return BC_ERR_ARG;
 

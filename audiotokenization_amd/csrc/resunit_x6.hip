@@ -479,19 +479,15 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
 // fragment reads per K32 unit, bit-identical outputs): 4-6 % per unit (profiles/r03m_ru_tiles.txt); x6 is
 // neutral there (7.05 vs 7.08 ms) and keeps 109.  The 48-row bf16 tiles with more columns per wave (106, 124)
 // need more than 128 VGPRs (one workgroup per CU) and run 1.8-2.1x slower than 111.
-static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 123, 124, 125, 126};
-static const int kRUCandidatesP12[] = {123, 109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 124, 125, 126};
+// Measured and not kept (round 4, profiles/r04d_resunit_w16_rejected.txt): the same units on 16-wave tiles, one
+// 1024-thread workgroup per CU (96 x 256 at C = 96: 5.76 -> 6.36 ms, 6.09 with four taps per K-step; 48 x 512 at
+// C = 48: 6.15 ms against the strip kernel's 4.52, with 14-28 spilled VGPRs): the kernel takes 16-wave tiles, the
+// table has none.
+static const int kRUCandidates[] = {109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 123, 124};
+static const int kRUCandidatesP12[] = {123, 109, 111, 110, 116, 112, 113, 117, 106, 104, 105, 124};
 constexpr size_t RU_LDS_MAX = 80 * 1024;
-// LDS budget of a candidate: two workgroups per CU for the 8-wave tiles, the whole CU for the 16-wave ones
+// LDS budget of a candidate: two workgroups per CU for the 8-wave tiles, the whole CU for 16-wave ones
 static size_t ru_lds_budget(const X6Tile& t) { return t.WM * t.WN == 16 ? 160 * 1024 : RU_LDS_MAX; }
-// BC_RU_W16=1 prefers the 16-wave tiles 125 / 126 (one 1024-thread workgroup per CU; A/B timing)
-static bool ru_w16() {
-  static const bool v = [] {
-    const char* e = getenv("BC_RU_W16");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
 // BC_RU_CFG forces one candidate tile (timing experiments; it must fit the 160 KiB of a CU).
 static int ru_forced_cfg() {
   static const int v = [] {
@@ -531,17 +527,15 @@ int resunit_select_cfg(int C, int d, int mode) {
   if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
-  for (int pass = ru_w16() ? 0 : 1; pass < 2; ++pass)
-    for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
-      const X6Tile& t = x6_tile(cfg);
-      if (x6_BM(t) != C) continue;
-      if (pass == 0 && t.WM * t.WN != 16) continue;  // BC_RU_W16: the 16-wave tiles first
-      if (d > RU_MAX_DIL) return -1;
-      int bp, hp;
-      const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
-      if (forced ? (cfg != forced || lds > 160 * 1024) : lds > ru_lds_budget(t)) continue;
-      return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
-    }
+  for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
+    const X6Tile& t = x6_tile(cfg);
+    if (x6_BM(t) != C) continue;
+    if (d > RU_MAX_DIL) return -1;
+    int bp, hp;
+    const size_t lds = ru_lds(t, C, d, P, &bp, &hp);
+    if (forced ? (cfg != forced || lds > 160 * 1024) : lds > ru_lds_budget(t)) continue;
+    return cfg + (P == 2 ? 200 : P == 1 ? 100 : 0);
+  }
   return -1;
 }
 
@@ -601,7 +595,7 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
   if (mode < 1 || mode > 3 || !resunit_cfg_ok(cfg, C, d)) return -1;
-  if (mode == 3 && cfg != 326 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
+  if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   return snprintf(buf, n, "resunit_x6_kernel<%d, %d, %d, %d, %d, %d>", t.MT, t.NT, t.WM, t.WN, P,
@@ -612,8 +606,7 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
                    const float* isa, const float* isb) {
-  // h3 at C = 48: the register-weight / strip kernels (not when a 16-wave one-launch tile is asked for, A/B timing)
-  if (cfg >= 300 && cfg < 400 && cfg != 326 && resunit_rr_ok(C, d)) {
+  if (cfg >= 300 && cfg < 400 && resunit_rr_ok(C, d)) {  // h3 at C = 48: the register-weight / strip kernels
     const int rc = resunit_rr_launch(x_raw, x_act, w7, b7, s2a, s2b, w1, b1, osa, osb, y, y2, B, C, T, d, pl, st,
                                      isa, isb);
     if (rc != BC_ERR_UNSUPPORTED) return rc;
@@ -651,8 +644,6 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
     BC_RU_CASES(17, 4, 1, 2, 4)
     BC_RU_CASES(23, 3, 2, 2, 4)
     BC_RU_CASES(24, 3, 4, 1, 8)
-    BC_RU_CASES(25, 3, 2, 2, 8)
-    BC_RU_CASES(26, 3, 2, 1, 16)
   }
 #undef BC_RU_CASES
   return BC_ERR_ARG;
