@@ -38,7 +38,8 @@ struct RUExtra {
   const float* s2b;  //                               inv_beta  [C]
   int hplane;        // bytes per Hs plane = nck1 * BN * 64
   int nck1;          // 32-channel chunks of the k=1 conv's input
-  int dbg;           // BC_RU_DEBUG timing experiments (wrong results): 1 no A copies, 2 no B loads, 4 no epilogue, 8 no phase 2
+  int dbg;           // BC_RU_DEBUG timing experiments (wrong results, BC_ABLATION builds only): 1 no A copies, 2 no B
+                     // loads, 4 no epilogue, 8 no phase 2, 16 no Snake on load, 32 no phase-1 MFMAs, 64 no bridge Snake
   // snake on load: the unit's first Activation1d applied while staging the k=7 input (x_act == x_raw,
   // isa / isb = its alpha_exp / inv_beta), so the producer writes only the raw tensor; nullptr: x_act given
   const float* isa;
@@ -168,7 +169,7 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
   // snake on load (r.isa): activate the thread's two staged channels of `chunk` in registers (out-of-range
   // loads read 0 and snake(0) = 0: the zero padding of the activated signal, as the reference pads it)
   auto activate_b = [&](int chunk) {
-    if (!r.isa) return;
+    if (!r.isa || BC_ABL(r.dbg, 16)) return;
     const int ci0 = chunk * X6_BKC + 2 * bp;
     const float a0 = ci0 < a.Cin ? r.isa[ci0] : 0.f, b0 = ci0 < a.Cin ? r.isb[ci0] : 0.f;
     const float a1 = ci0 + 1 < a.Cin ? r.isa[ci0 + 1] : 0.f, b1 = ci0 + 1 < a.Cin ? r.isb[ci0 + 1] : 0.f;
@@ -257,6 +258,7 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
       for (int tt = 0; tt < TPS; ++tt) {
       const int tap = tp * TPS + tt;
       if (TPS > 1 && tap >= K) break;
+      if (BC_ABL(r.dbg, 32)) break;
       const unsigned char* Ab = As + (step & 1) * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
       const unsigned char* Bcol = Bs + bgrp(col_lane + tap * a.d, lane >> 4);
       frag_t bf[NT][P];
@@ -355,7 +357,8 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
         const f32x2 sa = {r.s2a[c0], r.s2a[c0 + 1]}, sb = {r.s2b[c0], r.s2b[c0 + 1]};
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          const f32x2 v = snake_pk((f32x2){acc[i][j][2 * pr], acc[i][j][2 * pr + 1]} * sc + bias, sa, sb);
+          const f32x2 pre = (f32x2){acc[i][j][2 * pr], acc[i][j][2 * pr + 1]} * sc + bias;
+          const f32x2 v = BC_ABL(r.dbg, 64) ? pre : snake_pk(pre, sa, sb);
           acc[i][j][2 * pr] = v.x;
           acc[i][j][2 * pr + 1] = v.y;
           const unsigned u0 = __float_as_uint(fabsf(v.x)), u1 = __float_as_uint(fabsf(v.y));

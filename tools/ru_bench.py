@@ -9,7 +9,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, REPO)
+# BIGCODEC_PKG_ROOT: import the package from another tree (an ablation build under gpurun_abl/)
+sys.path.insert(0, os.environ.get("BIGCODEC_PKG_ROOT", REPO))
 
 import torch  # noqa: E402
 
