@@ -377,7 +377,7 @@ int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n) {
   // (the 16-byte staging also needs Tin % 4 == 0 and 16-B aligned rows at launch, x6_b4_fits: true of every
   // BigCodec shape at the configs' clip lengths; a launch that fails it runs the single-float variant)
   const int T4 = P == 1 ? 4 : P == 2 ? 2 : 1;
-  const bool b4 = v.b4 && v.tps == T4 && v.db == (P == 1);
+  const bool b4 = v.b4 && (v.pw || (v.tps == T4 && v.db == (P == 1)));
   return snprintf(buf, n, "conv1d_x6_kernel<%d, %d, %d, %d, %d, %s, %d, %s, %s>", t.MT, t.NT, t.WM, t.WN, P,
                   v.pw ? "true" : "false", v.tps, v.db ? "true" : "false", b4 ? "true" : "false");
 }

@@ -59,9 +59,9 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
   static_assert(NW == 8 || NW == 16, "512- or 1024-thread workgroups");
   constexpr int NCG = NW / 8;  // B staging column groups (16 channel pairs x 32 column lanes each)
   constexpr int CI = ((PW ? BN / 32 : X6_MAXCOL_ITERS) + NCG - 1) / NCG;  // 32-column B passes per thread
-  static_assert(!(B4 && PW), "16-byte staging is for the multi-tap path");
   constexpr int NQI = 4 * NW;  // B4: column quads per iteration (NW / 2 quad blocks of 8, 2 pair blocks of 8)
-  constexpr int IT4 = ((32 * X6_MAXCOL_ITERS + 6) / 4 + NQI - 1) / NQI;  // B4 iterations: ncol + 3 <= 4 * NQI * IT4
+  // B4 iterations: ncol + 3 <= 4 * NQI * IT4 (pointwise: the input tile is the BN aligned columns)
+  constexpr int IT4 = PW ? (BN / 4 + NQI - 1) / NQI : ((32 * X6_MAXCOL_ITERS + 6) / 4 + NQI - 1) / NQI;
   constexpr int NBL = B4 ? 2 * IT4 : 2 * CI;  // B load instructions per thread and chunk (the counted waits)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
   __shared__ unsigned smax[2][NW];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
@@ -371,28 +371,50 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     // Pointwise conv (K = 1): one step per chunk, so the B loads run two chunks ahead in two
     // register sets (chunk c + 2 is issued while chunk c computes and chunk c + 1 is stored).
     float bw0[CI], bw1[CI];
-    if (a.nchunks > 1) load_b(1, bw0, bw1);
-    auto step1 = [&](int c, const float (&n0v)[CI], const float (&n1v)[CI], float (&p0v)[CI], float (&p1v)[CI]) {
+    floatx4 bx0[B4 ? IT4 : 1], bx1[B4 ? IT4 : 1];  // B4: the second register set
+    // the staging steps on a register set of the variant (float[CI] pairs or, B4, floatx4[IT4] pairs)
+    auto ld = [&](int chunk, auto& v0, auto& v1) {
+      if constexpr (B4) load_b4(chunk, v0, v1);
+      else load_b(chunk, v0, v1);
+    };
+    auto mx = [&](auto& v0, auto& v1, int par) {
+      if constexpr (B4) bmax_publish4(v0, v1, par);
+      else bmax_publish(v0, v1, par);
+    };
+    auto st = [&](auto& v0, auto& v1) {
+      if constexpr (B4) store_b4(v0, v1, Bs, xs);
+      else store_b(v0, v1, Bs, xs);
+    };
+    auto step1 = [&](int c, auto& n0v, auto& n1v, auto& p0v, auto& p1v) {
       if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
       dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
-      if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) load_b(c + 2, p0v, p1v);
+      if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);
       compute(c & 1, 0, 0);
       if (c + 1 < a.nchunks) {
-        if constexpr (P == 2) bmax_publish(n0v, n1v, (c + 1) & 1);
+        if constexpr (P == 2) mx(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
         if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-        if (!BC_ABL(a.dbg, 4)) store_b(n0v, n1v, Bs, xs);
+        if (!BC_ABL(a.dbg, 4)) st(n0v, n1v);
       }
-      // the A copy of step c + 1 (issued before the 2*CI loads of chunk c + 2) must have landed
+      // the A copy of step c + 1 (issued before the NBL loads of chunk c + 2) must have landed
       if (c + 2 < a.nchunks)
-        wait_vmcnt<2 * CI>();
+        wait_vmcnt<NBL>();
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
     };
-    for (int c = 0; c < a.nchunks; c += 2) {
-      step1(c, bw0, bw1, bv0, bv1);
-      if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
+    if constexpr (B4) {
+      if (a.nchunks > 1) ld(1, bx0, bx1);
+      for (int c = 0; c < a.nchunks; c += 2) {
+        step1(c, bx0, bx1, bq0, bq1);
+        if (c + 1 < a.nchunks) step1(c + 1, bq0, bq1, bx0, bx1);
+      }
+    } else {
+      if (a.nchunks > 1) ld(1, bw0, bw1);
+      for (int c = 0; c < a.nchunks; c += 2) {
+        step1(c, bw0, bw1, bv0, bv1);
+        if (c + 1 < a.nchunks) step1(c + 1, bv0, bv1, bw0, bw1);
+      }
     }
   } else {
     const bool prio = BC_ABL(a.dbg, 16);
@@ -572,7 +594,10 @@ inline X6Variant x6_variant_base(const X6Tile& t, int P, int K, int s, int d) {
 // ps: the phase factor of a phase-decomposed strided conv (its rows gather s phases: no 16-byte staging)
 inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d, int ps = 0) {
   X6Variant v = x6_variant_base(t, P, K, s, d);
-  v.b4 = !v.pw && s == 1 && ps == 0 && t.WM * t.WN == 16 && x6_b4_on();
+  // 16-byte staging: the 16-wave tile's multi-tap launches, and the pointwise launches of the 16-wave tile and of
+  // the 192 x 128 tile (whose 32-quad iteration covers its 128 columns)
+  const bool pw_tile = t.WM * t.WN == 16 || (t.MT == 6 && t.NT == 2 && t.WM == 2 && t.WN == 4);
+  v.b4 = s == 1 && ps == 0 && x6_b4_on() && (v.pw ? pw_tile : t.WM * t.WN == 16);
   return v;
 }
 inline bool x6_b4_fits(const ConvArgs& a) {
@@ -619,6 +644,13 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   if constexpr (P == 1 && WM * WN == 16) {
     if (v.tps == 4) {
       hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, 4, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
+      BC_CHECK_LAUNCH();
+      return BC_OK;
+    }
+  }
+  if constexpr (WM * WN == 16 || (MT == 6 && NT == 2 && WM == 2 && WN == 4)) {
+    if (v.pw && v.b4 && x6_b4_fits(a)) {
+      hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, true, 1, false, true>), dim3(a.nwg), dim3(NTHR), v.lds, st, a);
       BC_CHECK_LAUNCH();
       return BC_OK;
     }

@@ -257,11 +257,11 @@ def test_kernel_names_come_from_the_launchers():
             planes = {1: 3, 2: 1, 3: 2}[base // 100]
             assert name.startswith(f"conv1d_x6_kernel<{mt}, {nt}, {wm}, {wn}, {planes}, "), (cfg, name)
             # <..., planes, pointwise, taps per K-step, double-buffered B, 16-byte input staging>
-            assert re.search(r", (true, 1, false, false|false, [124], (true|false), (true|false))>$", name), name
+            assert re.search(r", (true, 1, false|false, [124], (true|false)), (true|false)>$", name), name
         else:
             mt, wm, nt, wn, bkc = L.CONV_CFGS[cfg]
             assert name == f"conv1d_mfma_kernel<{mt}, {wm}, {nt}, {wn}, {bkc}>", name
-    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false, false>")  # pointwise
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 1, 1, 1, 3), 1).endswith("true, 1, false, true>")  # pointwise, B4
     # k7 C = 768: the 16-wave 192 x 256 tile, two taps per K-step, 16-byte input staging; the final k3 keeps the
     # double-buffered 256 x 256; the phase-decomposed stride-5 conv on the 16-wave tile stages single floats
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 768, 7, 1, 3, 3), 7, 1, 3) == \

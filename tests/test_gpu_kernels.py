@@ -812,3 +812,46 @@ def test_reslstm_bidirectional(dev, D, layers, B, T):
     with pytest.raises(NotImplementedError):
         m.run(x.to(dev), return_state=True)
     assert L.load().bc_lstm_status(1) == 0
+
+
+@pytest.mark.parametrize("Cin,Cout,K,d,T,cfg", [
+    (192, 192, 7, 3, 1200, 322), (384, 384, 7, 9, 700, 322), (192, 192, 7, 1, 2000, 222), (192, 192, 7, 3, 1200, 122),
+    (384, 384, 1, 1, 1000, 314), (192, 192, 1, 1, 1000, 322), (768, 768, 1, 1, 520, 214), (384, 384, 1, 1, 1000, 114),
+    (384, 384, 1, 1, 1000, 122)])
+def test_b4_staging_bit_identical_to_single_float(dev, Cin, Cout, K, d, T, cfg):
+    """16-byte input staging (B4: stride-1 launches whose rows are 16-byte aligned with Tin % 4 == 0) stages the
+    same values, block maxima and LDS image as the single-float staging, which runs when the input is not 16-byte
+    aligned: an aligned and a 4-byte-offset copy of the same input give bit-identical outputs (k7 16-wave tiles,
+    pointwise 192 x 128 and 16-wave tiles; h3, bf16, x6), within the conv tolerance of the oracle in h3 / x6."""
+    prec = {1: "x6", 2: "bf16", 3: "h3"}[cfg // 100]
+    old = L.precision_mode()
+    L.set_precision(prec)
+    try:
+        g = torch.Generator().manual_seed(Cin + Cout * 3 + K + d)
+        pad = K // 2 * d
+        m = CV.WNConv1d(Cin, Cout, kernel_size=K, dilation=d, padding=pad)
+        conv = _rand_wn_conv(m, g)
+        B = 2
+        x = torch.randn(B, Cin, T, generator=g)
+        res = torch.randn(B, Cout, T, generator=g)
+        sd = {k: v.detach() for k, v in conv.state_dict().items()}
+        want = O.conv(x, sd, "", K, 1, pad, d, False) + res
+        m.to(dev)
+        st = torch.cuda.current_stream().cuda_stream
+        wp, bias = m.packed_as(cfg, dev)
+        buf = torch.empty(B * Cin * T + 4, device=dev)
+        outs = []
+        for off in (0, 1):  # the allocation is 256-B aligned: offset 0 takes B4, offset 1 float the single-float path
+            xd = buf[off:off + B * Cin * T].view(B, Cin, T)
+            xd.copy_(x.to(dev))
+            rd = res.to(dev)
+            y = torch.empty(B, Cout, T, device=dev)
+            L.call("bc_conv1d_fwd", xd.data_ptr(), wp.data_ptr(), L.ptr(bias), rd.data_ptr(), 0, 0, y.data_ptr(), 0,
+                   B, Cin, T, Cout, T, K, 1, d, pad, 0, cfg, st)
+            torch.cuda.synchronize()
+            outs.append(y.cpu())
+        assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+        tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if prec != "bf16" else 2e-2
+        assert_close_rel(outs[0], want, tol, f"{prec} cfg {cfg}")
+    finally:
+        L._mode = old
