@@ -422,6 +422,23 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
       *reinterpret_cast<u32x2_t*>(dst + 2 * r.hplane) = (u32x2_t){l0, l1};
     }
   }
+  // the epilogue's residual (the unit's skip input x_raw): the 16-byte groups of the tiles this wave finishes in
+  // phase 2, issued once h is in LDS (the accumulators are dead: no spills) so they land under phase 2 (the epilogue
+  // loaded them itself: one exposed HBM round trip per workgroup, 20 % of a C = 96 unit in the round-4 ablation,
+  // profiles/r04e_ru_ablation.txt)
+  floatx4 rpre[NTW];
+  {
+    const float* rb = e.res ? e.res + (long long)b * e.rbs : nullptr;
+    const int co = mq * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int nb = n0 + (jg * NTW + j) * 16 + (lane >> 4) * 4;
+      rpre[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (p2 && rb && e.vec && co < e.Cout && nb + 3 < e.Nout &&
+          BC_DOK((long long)co * e.yT + e.ooff + nb + 3 < e.rbs))
+        rpre[j] = *reinterpret_cast<const floatx4*>(rb + (long long)co * e.yT + e.ooff + nb);
+    }
+  }
   lds_barrier();
 
   // ---------------- phase 2: y = conv1(h_act), input as the MFMA A operand ----------------
@@ -464,7 +481,7 @@ __global__ void __launch_bounds__(64 * WM * WN, ru_launch_waves(MT, NT, WM, WN, 
     if (BC_ABL(r.dbg, 4)) {
       if (acc2[0][0][0] == 1234.5f) e.y[0] = 0.f;  // keep the MFMAs alive
     } else {
-      conv_epilogue<1, NTW, P == 2>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs);
+      conv_epilogue_res<NTW, P == 2>(e, acc2, b, mq * 16, n0 + jg * NTW * 16, lane, 1.f / hs, rpre);
     }
   }
 }
