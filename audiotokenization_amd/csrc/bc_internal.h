@@ -27,7 +27,6 @@ struct ConvArgs {
   int vec;             // 16-byte epilogue accesses allowed (conv_epilogue_vec_ok)
   int nchunks, win, bstage, astage;
   int bpitch;          // x6 kernel: bytes per B-tile column per plane (64: swizzled, stride 1; 80: strided)
-  int fe;              // x6 kernel, 16-wave tile: epilogue fused into the last K32 unit (x6_fe_on)
   float inv_win;
   int ntm, ntn, nwg;
 };

@@ -22,8 +22,6 @@
 //                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
 //                at tap 0 and land while the current chunk's taps compute.
 #pragma once
-#include <type_traits>
-
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
@@ -281,23 +279,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
 
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
 
-  // Fused epilogue (FE: the 16-wave tile's multi-tap launches): the launch's last K32 unit finishes m-tile i - 1
-  // (bias, scale, Snake / tanh, stores) right after issuing m-tile i's MFMAs, so the epilogue's VALU and stores run
-  // under the matrix pipe instead of after it (the epilogue was 9-21 % of these launches in the round-4 ablation,
-  // profiles/r04h_strided_ablation.txt).  Same arithmetic per element: outputs bit-identical.
-  constexpr bool FE_T = !PW && WM * WN == 16;
-  const bool FE = FE_T && a.fe;  // ConvArgs::fe: BC_X6_FE=0 keeps the separate epilogue (A/B timing)
-  auto finish = [&](int i) {
-    const floatx4 (&acci)[1][NT] = *reinterpret_cast<const floatx4 (*)[1][NT]>(&acc[i]);
-    if constexpr (P == 2)
-      conv_epilogue<1, NT, true>(a, acci, b, m0 + wm * MT * 16 + i * 16, n0 + wn * NT * 16, lane, 1.f / xs);
-    else
-      conv_epilogue<1, NT>(a, acci, b, m0 + wm * MT * 16 + i * 16, n0 + wn * NT * 16, lane);
-  };
-  // one K32 unit: this wave's MT x NT tiles += A(buffer buf, slot tt) * B(tap-shifted columns); fin (a
-  // std::bool_constant): the launch's last unit, which also finishes the tiles (FE)
-  auto compute = [&](int buf, int tt, int tap, auto fin) {
-      constexpr bool FIN = decltype(fin)::value;
+  // one K32 unit: this wave's MT x NT tiles += A(buffer buf, slot tt) * B(tap-shifted columns)
+  auto compute = [&](int buf, int tt, int tap) {
       const unsigned char* Ab = As + buf * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
       // (n-tile j adds 16 * s columns: the swizzle of a stride-1 tile repeats every 8 columns)
       const unsigned char* Bcol = Br + bgrp(col_lane + tap * a.d, lane >> 4);
@@ -369,12 +352,6 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
             acc[i][j] = t;
           }
         }
-        if constexpr (FIN) {
-          if (i > 0 && !BC_ABL(a.dbg, 8)) finish(i - 1);  // m-tile i - 1 is final while m-tile i's MFMAs run
-        }
-      }
-      if constexpr (FIN) {
-        if (!BC_ABL(a.dbg, 8)) finish(MT - 1);
       }
   };
 
@@ -412,7 +389,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
       dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
       if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);
-      compute(c & 1, 0, 0, std::false_type{});
+      compute(c & 1, 0, 0);
       if (c + 1 < a.nchunks) {
         if constexpr (P == 2) mx(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
@@ -456,16 +433,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
 #pragma unroll
         for (int tt = 0; tt < TPS; ++tt) {
           const int tap = tp * TPS + tt;
-          if (TPS == 1 || tap < K) {
-            if constexpr (FE_T) {
-              if (FE && step == nsteps - 1 && tap == K - 1)
-                compute(step & 1, tt, tap, std::true_type{});
-              else
-                compute(step & 1, tt, tap, std::false_type{});
-            } else {
-              compute(step & 1, tt, tap, std::false_type{});
-            }
-          }
+          if (TPS == 1 || tap < K) compute(step & 1, tt, tap);
         }
         if (prio) __builtin_amdgcn_s_setprio(0);
         if constexpr (DB) {
@@ -490,7 +458,6 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
         // step 0 of a multi-step chunk the NBL B loads of the next chunk were issued after it and
         // may stay in flight (vmcnt retires in issue order); they are consumed at the chunk's last
         // step, where the compiler waits for their registers itself.
-        if (FE && step == nsteps - 1) break;  // finished in the last unit: no wait, no barrier before the exit
         if (tp == 0 && kst > 1 && c + 1 < a.nchunks)
           wait_vmcnt<NBL>();
         else
@@ -501,7 +468,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     }
   }
 
-  if (!FE && !BC_ABL(a.dbg, 8)) {
+  if (!BC_ABL(a.dbg, 8)) {
     if constexpr (P == 2)
       conv_epilogue<MT, NT, true>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
     else
@@ -633,14 +600,6 @@ inline X6Variant x6_variant(const X6Tile& t, int P, int K, int s, int d, int ps 
   v.b4 = s == 1 && ps == 0 && x6_b4_on() && (v.pw ? pw_tile : t.WM * t.WN == 16);
   return v;
 }
-// BC_X6_FE=0 keeps the 16-wave tile's epilogue after its last K-step (A/B timing of the fused epilogue).
-inline bool x6_fe_on() {
-  static const bool v = [] {
-    const char* e = getenv("BC_X6_FE");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
 inline bool x6_b4_fits(const ConvArgs& a) {
   return a.ps == 0 && a.s == 1 && a.Tin % 4 == 0 && a.xbs % 4 == 0 && ((unsigned long long)a.x & 15) == 0;
 }
@@ -668,7 +627,6 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
   const size_t lds = x6_lds(t, ncol, P, a.s);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   const X6Variant v = x6_variant(t, P, a.K, a.s, a.d, a.ps);
-  a.fe = x6_fe_on() ? 1 : 0;
   constexpr int T2 = P <= 2 ? 2 : 1;
   constexpr bool D2 = P <= 2;
   if constexpr (WM * WN == 16) {  // 16-byte input staging: the 16-wave tile's multi-tap variant of each precision
