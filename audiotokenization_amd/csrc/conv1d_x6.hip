@@ -130,12 +130,13 @@ static int x6_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 //   1: stride-1 multi-tap convs with Cout % 192 == 0 instead of the 8-wave 120
 //   2: the phase-decomposed strided convs with Cout % 192 == 0 instead of 120
 //   4: the k7 C = 768 convs instead of the 256 x 256 tile 121
-//   8: the pointwise C = 192 convs instead of 114
+//   8: the pointwise C = 192 convs instead of 114 (off by default since the 16-byte staging: 114 2.99 vs 3.08 ms in
+//      h3 and 2.70 vs 2.78 in bf16 with residual + dual output, profiles/r04j_pw_tiles.txt)
 //  16: the pointwise Cout >= 2048 convs (the LSTM input projection) instead of the 256 x 256 tile 121
 static int x6_w16() {
   static const int v = [] {
     const char* e = getenv("BC_X6_W16");
-    return e ? atoi(e) : 31;
+    return e ? atoi(e) : 23;
   }();
   return v;
 }
