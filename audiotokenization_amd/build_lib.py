@@ -63,7 +63,7 @@ def _digest(flags=None) -> str:
             h.update(fh.read())
     with open(os.path.join(REPO, "include", "bigcodec.h"), "rb") as fh:
         h.update(fh.read())
-    h.update(" ".join(flags or CFLAGS).encode())
+    h.update(" ".join(flags or CFLAGS).replace(REPO, "<repo>").encode())  # (the tree moves: gpurun, the driver)
     return h.hexdigest()
 
 

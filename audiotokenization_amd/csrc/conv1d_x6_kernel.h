@@ -633,7 +633,7 @@ static int launch_x6(ConvArgs& a, int B, hipStream_t st) {
     if (v.b4 && x6_b4_fits(a)) {
       constexpr int T4 = P == 1 ? 4 : P == 2 ? 2 : 1;
       constexpr bool D4 = P == 1;  // the k7 variants: bf16 4 taps over two B buffers, h3 2 taps, x6 1
-      if (v.tps == T4 && v.db == D4) {
+      if (!v.pw && v.tps == T4 && v.db == D4) {  // (x6 pointwise launches also have tps 1, no DB: the PW path below)
         hipLaunchKernelGGL((conv1d_x6_kernel<MT, NT, WM, WN, P, false, T4, D4, true>), dim3(a.nwg), dim3(NTHR), v.lds,
                            st, a);
         BC_CHECK_LAUNCH();
