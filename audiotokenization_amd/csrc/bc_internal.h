@@ -27,6 +27,7 @@ struct ConvArgs {
   int vec;             // 16-byte epilogue accesses allowed (conv_epilogue_vec_ok)
   int nchunks, win, bstage, astage;
   int bpitch;          // x6 kernel: bytes per B-tile column per plane (64: swizzled, stride 1; 80: strided)
+  int prio;            // x6 kernel, 16-wave tile: s_setprio(1) for waves 8-15 for the whole launch (BC_X6_PRIO, A/B)
   float inv_win;
   int ntm, ntn, nwg;
 };
