@@ -173,8 +173,18 @@ class BigCodecDecoder(nn.Module):
     def tokens_to_audio(self, vq):
         """Token -> audio: codes (B, T, Nq) int64 on the device (extract_indices' (F, Nq) files, batched)
         -> waveform (B, 1, T * hop): vq2emb (codec_decoder.py:96-99) -> transpose(1, 2) -> self(x, vq=False),
-        with the embedding written straight in the decoder's (B, D, T) layout (bc_vq2emb_ct)."""
-        return self.decode(self.quantizer.vq2emb_ct(vq))
+        with the embedding written straight in the decoder's (B, D, T) layout (bc_vq2emb_ct).  fsq=True decoders
+        (whose vq2emb raises AttributeError in the reference: FSQ has none) take one index column through
+        FSQ.indices_to_codes (finite_scalar_quantization.py:176-192, bc_fsq_codes), then the same decode."""
+        return self.decode(self.tokens_to_latent(vq))
+
+    def tokens_to_latent(self, vq):
+        """codes (B, T, Nq) on the device -> the decoder's input (B, D, T) (see tokens_to_audio)."""
+        if self.fsq:
+            if vq.dim() != 3 or vq.shape[2] != 1:
+                raise ValueError(f"an fsq=True decoder takes (B, T, 1) indices, got {tuple(vq.shape)}")
+            return self.quantizer.indices_to_codes(vq[:, :, 0])
+        return self.quantizer.vq2emb_ct(vq)
 
     def inference_vq(self, vq):
         return self.decode(vq[None, :, :])

@@ -494,6 +494,11 @@ int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float
   return fsq_fwd_launch(z, w_in, b_in, w_out, b_out, consts, idx, post, B, D, T, d, S(stream));
 }
 
+int bc_fsq_codes(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
+                 float* post, int B, int D, int T, int d, void* stream) {
+  return fsq_codes_launch(idx, idx_bits, levels, w_out, b_out, post, B, D, T, d, S(stream));
+}
+
 int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const float* w_out,
                  const float* b_out, float* emb, int B, int T, int D, int n_codes, int dim, void* stream) {
   if (dim != 8) return BC_ERR_UNSUPPORTED;

@@ -117,6 +117,8 @@ int resample_sinc_launch(const float* x, float* y, const float* kern, int B, lon
                          long long ypitch, int orig, int nw, int K, int width, hipStream_t st);
 int fsq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* w_out, const float* b_out,
                    const float* consts, int* idx, float* post, int B, int D, int T, int nd, hipStream_t st);
+int fsq_codes_launch(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
+                     float* post, int B, int D, int T, int nd, hipStream_t st);
 int vq2emb_ct_launch(const long long* idx, int nq, const float* cb, const float* w_out, const float* b_out,
                      float* emb, int B, int T, int D, int n_codes, hipStream_t st);
 int vq2emb_launch(const long long* idx, long long idx_stride, const float* cb, const float* w_out,

@@ -385,6 +385,22 @@ Tensor vq2emb_ct(const Tensor& idx, const Tensor& cbs, const Tensor& w_out, cons
   return out;
 }
 
+Tensor fsq_codes(const Tensor& idx, const Tensor& w_out, const Tensor& b_out, at::IntArrayRef levels) {
+  TORCH_CHECK_VALUE(idx.is_cuda() && (idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong) &&
+                        idx.is_contiguous(),
+                    "bigcodec::fsq_codes: idx must be a contiguous int32 / int64 device tensor");
+  TORCH_CHECK_VALUE(idx.dim() == 2, "bigcodec::fsq_codes: idx must be (B, T)");
+  const int64_t B = idx.size(0), T = idx.size(1), d = (int64_t)levels.size(), D = b_out.numel();
+  TORCH_CHECK_VALUE(d >= 1 && d <= 8 && w_out.numel() == D * d, "bigcodec::fsq_codes: parameter shapes");
+  std::vector<int> lv(levels.begin(), levels.end());
+  auto post = at::empty({B, D, T}, idx.options().dtype(at::kFloat));
+  ok(bc_fsq_codes(idx.data_ptr(), idx.scalar_type() == at::kLong ? 64 : 32, lv.data(), req(idx, w_out, "w_out"),
+                  req(idx, b_out, "b_out"), post.data_ptr<float>(), i32(B, "B"), i32(D, "D"), i32(T, "T"), (int)d,
+                  stream_of(idx)),
+     "bc_fsq_codes");
+  return post;
+}
+
 std::vector<Tensor> fsq(const Tensor& z, const Tensor& w_in, const Tensor& b_in, const Tensor& w_out, const Tensor& b_out,
                         const Tensor& consts) {
   dev(z, "z");
@@ -465,6 +481,7 @@ TORCH_LIBRARY(bigcodec, m) {
   m.def("rvq_update_(Tensor(a!) residual, Tensor(b!) out, Tensor q, bool first) -> ()");
   m.def("vq2emb_ct(Tensor idx, Tensor codebooks, Tensor w_out, Tensor b_out) -> Tensor");
   m.def("fsq(Tensor z, Tensor w_in, Tensor b_in, Tensor w_out, Tensor b_out, Tensor consts) -> Tensor[]");
+  m.def("fsq_codes(Tensor idx, Tensor w_out, Tensor b_out, int[] levels) -> Tensor");
   m.def("resample_sinc(Tensor x, Tensor kern, int lout, int pitch, int orig, int new_freq, int taps, int width) -> Tensor");
   m.def("synth_clips_(Tensor(a!) x, int clip0) -> ()");
 }
@@ -487,6 +504,7 @@ TORCH_LIBRARY_IMPL(bigcodec, CUDA, m) {
   m.impl("rvq_update_", &Guarded<&rvq_update_>::call);
   m.impl("vq2emb_ct", &Guarded<&vq2emb_ct>::call);
   m.impl("fsq", &Guarded<&fsq>::call);
+  m.impl("fsq_codes", &Guarded<&fsq_codes>::call);
   m.impl("resample_sinc", &Guarded<&resample_sinc>::call);
   m.impl("synth_clips_", &Guarded<&synth_clips_>::call);
 }

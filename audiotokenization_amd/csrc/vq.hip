@@ -9,6 +9,7 @@
 //  vq2emb_kernel              : indices -> out_proj(codebook[idx]) (:78-91, residual_vq.py:42-48).
 //  vq2emb_ct_kernel           : the token -> audio entry: stacked quantizers, (B, D, T) output.
 //  fsq_fwd_kernel             : the FSQ quantizer (fsq=True decoders).
+//  fsq_codes_kernel           : FSQ indices -> project_out(codes) (the fsq=True token -> latent step).
 //
 // Bit-exactness contract (tests/test_vq_*): given the same z_e, the indices equal the reference's.
 // The fp32 operation order below restates what torch's CPU kernels do for these shapes, verified
@@ -262,6 +263,77 @@ int fsq_fwd_launch(const float* z, const float* w_in, const float* b_in, const f
   if (nwg > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(fsq_fwd_kernel, dim3((unsigned)nwg), dim3(256), 0, st, z, w_in, b_in, w_out, b_out, consts, idx,
                      post, B, D, T, nd);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+// FSQ token -> latent (finite_scalar_quantization.py:159-192 indices_to_codes, channel_first, one codebook; the
+// fsq=True decoder's inverse of forward's indices): idx[B][T] (int32 or int64) -> post[B][D][T] = project_out(codes).
+//   lvl[j]  = floor(idx / basis[j]) mod levels[j]  (torch's // and % on integers: floor division, non-negative
+//             modulo, so any integer maps to a grid point exactly as the reference maps it, :170-174)
+//   code[j] = float(lvl[j] - hw[j]) / float(hw[j])  (_scale_and_shift_inverse, :155-157: integer difference,
+//             true division in fp32)
+//   post    = fsq_fwd_kernel's project_out chain (fma over j from 0, + b_out), so an index forward produced
+//             decodes to forward's own post bit for bit (its q is the integer lvl - hw).
+// Thread = one position t, the workgroup walks FSQ_CT_D channels (stores coalesced along t).
+constexpr int FSQ_CT_D = 32;
+struct FsqLevels {
+  long long basis[FSQ_MAXD];
+  int levels[FSQ_MAXD];
+};
+__global__ void __launch_bounds__(256) fsq_codes_kernel(const void* __restrict__ idx, int idx64, FsqLevels lv, int nd,
+                                                        const float* __restrict__ w_out, const float* __restrict__ b_out,
+                                                        float* __restrict__ post, int T, int D) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int d0 = blockIdx.y * FSQ_CT_D;
+  const int b = blockIdx.z;
+  if (t >= T) return;
+  const long long n = (long long)b * T + t;
+  const long long k = idx64 ? static_cast<const long long*>(idx)[n] : (long long)static_cast<const int*>(idx)[n];
+  float code[FSQ_MAXD];
+#pragma unroll
+  for (int j = 0; j < FSQ_MAXD; ++j) {
+    code[j] = 0.f;
+    if (j < nd) {
+      const long long bs = lv.basis[j], L = lv.levels[j];
+      long long qd = k / bs;
+      if ((k % bs != 0) && ((k < 0) != (bs < 0))) --qd;  // floor division
+      long long m = qd % L;
+      if (m < 0) m += L;                                   // floor modulo (L > 0)
+      const long long hw = L / 2;
+      code[j] = (float)(m - hw) / (float)hw;
+    }
+  }
+  float* out = post + ((long long)b * D + d0) * T + t;
+  const int dn = D - d0 < FSQ_CT_D ? D - d0 : FSQ_CT_D;
+  for (int dd = 0; dd < dn; ++dd) {
+    const int c = d0 + dd;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < FSQ_MAXD; ++j)
+      if (j < nd) acc = fmaf(w_out[c * nd + j], code[j], acc);
+    out[(long long)dd * T] = acc + b_out[c];
+  }
+}
+
+int fsq_codes_launch(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
+                     float* post, int B, int D, int T, int nd, hipStream_t st) {
+  if (!idx || !levels || !w_out || !b_out || !post || B < 0 || D < 1 || T < 0 || nd < 1) return BC_ERR_ARG;
+  if (idx_bits != 32 && idx_bits != 64) return BC_ERR_ARG;
+  if (nd > FSQ_MAXD) return BC_ERR_UNSUPPORTED;
+  FsqLevels lv{};
+  long long basis = 1;
+  for (int j = 0; j < nd; ++j) {
+    if (levels[j] < 2) return BC_ERR_ARG;  // hw = levels // 2 divides
+    lv.levels[j] = levels[j];
+    lv.basis[j] = basis;                   // cumprod([1] + levels[:-1]) (:76-77)
+    basis *= levels[j];
+    if (basis > (1LL << 40)) return BC_ERR_UNSUPPORTED;
+  }
+  if (B == 0 || T == 0) return BC_OK;
+  if (B > 65535 || (D + FSQ_CT_D - 1) / FSQ_CT_D > 65535) return BC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(fsq_codes_kernel, dim3((T + 255) / 256, (D + FSQ_CT_D - 1) / FSQ_CT_D, B), dim3(256), 0, st, idx,
+                     idx_bits == 64 ? 1 : 0, lv, nd, w_out, b_out, post, T, D);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

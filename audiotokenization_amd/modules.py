@@ -529,3 +529,16 @@ class FSQ(nn.Module):
         w_in, b_in, w_out, b_out, consts = self.prepared(z.device)
         post, idx = _ops().fsq(z, w_in, b_in, w_out, b_out, consts)
         return post, idx
+
+    def indices_to_codes(self, indices):
+        """finite_scalar_quantization.py:176-192 for the decoder's FSQ (channel_first, one codebook): indices
+        (B, T) int32 / int64 on the device -> project_out(codes) (B, D, T), one bc_fsq_codes launch (torch's
+        floor // and % included: any integer maps to a grid point, as in the reference)."""
+        if indices is None:
+            raise AssertionError  # the reference's `assert exists(indices)`
+        if not self.channel_first or indices.dim() != 2:
+            raise NotImplementedError("FSQ.indices_to_codes on the HIP path takes (B, T) indices, channel_first")
+        if indices.device.type != "cuda":
+            raise L.BigCodecLibraryError("FSQ.indices_to_codes takes device index tensors")
+        w_in, b_in, w_out, b_out, consts = self.prepared(indices.device)
+        return _ops().fsq_codes(indices.contiguous(), w_out, b_out, self.levels)

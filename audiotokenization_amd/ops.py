@@ -25,7 +25,7 @@ _ns = None
 
 # every op the extension defines (tests check the registry against this list)
 OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "aa_snake_ex", "tanh", "reslstm", "reslstm_bidir", "vq_prepare_codebook", "vq",
-       "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "resample_sinc", "synth_clips_")
+       "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "fsq_codes", "resample_sinc", "synth_clips_")
 
 
 def load():
@@ -139,6 +139,11 @@ def _register_fakes():
     def _fsq(z, w_in, b_in, w_out, b_out, consts):
         B, D, T = z.shape
         return [_new(z, z.shape), _new(z, (B, T), torch.int32)]
+
+    @reg("bigcodec::fsq_codes")
+    def _fsq_codes(idx, w_out, b_out, levels):
+        B, T = idx.shape
+        return _new(idx, (B, b_out.shape[0], T), torch.float32)
 
     @reg("bigcodec::resample_sinc")
     def _resample(x, kern, lout, pitch, orig, new_freq, taps, width):

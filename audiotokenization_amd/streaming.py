@@ -152,7 +152,7 @@ class StreamingDecoder(StreamingEncoder):
 
     def tokens(self, codes) -> torch.Tensor:
         """codes (B, n, Nq) int64 on the device -> waveform chunk (B, 1, n * hop)."""
-        return self.push(self.decoder.quantizer.vq2emb_ct(codes))
+        return self.push(self.decoder.tokens_to_latent(codes))
 
     def _push_dec(self, z) -> torch.Tensor:
         z = _as_input(z)

@@ -69,7 +69,8 @@ def decode_index_files(decoder, paths: Iterable[str], device, batch: int = 16) -
     change its last frames through the decoder's receptive field, and the reference decodes each file
     on its own."""
     paths = list(paths)
-    n_codes = decoder.quantizer.layers[0].codebook_size
+    q = decoder.quantizer
+    n_codes = q.codebook_size if getattr(decoder, "fsq", False) else q.layers[0].codebook_size
     arrs = [load_indices(p) for p in paths]
     groups: dict = {}
     for i, a in enumerate(arrs):

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 12
+#define BC_ABI_VERSION 13
 
 int bc_abi_version(void);
 
@@ -249,6 +249,16 @@ int bc_vq2emb_ct(const long long* idx, int nq, const float* codebooks, const flo
  *   expressions); 1 <= d <= 8. */
 int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float* w_out, const float* b_out,
                const float* consts, int* idx, float* post, int B, int D, int T, int d, void* stream);
+
+/* bc_fsq_codes: FSQ.indices_to_codes (finite_scalar_quantization.py:159-192), channel_first, one codebook: the
+ *   fsq=True decoder's token -> latent step (its vq2emb raises AttributeError in the reference: FSQ has no vq2emb,
+ *   codec_decoder.py:96-99).  idx[B][T] (idx_bits 32: int32, 64: int64) -> post[B][D][T] = project_out(codes),
+ *   codes[j] = ((idx // basis[j]) % levels[j] - levels[j] // 2) / (levels[j] // 2) with torch's floor // and %
+ *   (any integer maps to a grid point, as in the reference), basis = cumprod([1] + levels[:-1]).  levels is a
+ *   HOST array of d ints >= 2; w_out [D][d], b_out [D] as in bc_fsq_fwd, whose post it reproduces bit for bit
+ *   for the indices it returned.  1 <= d <= 8. */
+int bc_fsq_codes(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
+                 float* post, int B, int D, int T, int d, void* stream);
 
 /* ---- Real-audio ingest ------------------------------------------------------------------------
  * bc_resample_sinc: torchaudio.transforms.Resample(orig, new) as extract_indices.py:129-132 and

@@ -281,6 +281,20 @@ def fsq_forward(z: Tensor, sd: SD, levels: Sequence[int], prefix: str = "quantiz
     return codes.transpose(1, 2), indices[..., 0]
 
 
+def fsq_indices_to_codes(indices: Tensor, sd: SD, levels: Sequence[int], prefix: str = "quantizer."):
+    """FSQ.indices_to_codes (finite_scalar_quantization.py:159-192) for the fsq=True decoder's quantizer
+    (channel_first, one codebook): indices (B, T) integer -> project_out(codes) (B, D, T).  Level indices by
+    torch's floor // and % (:170-174), so any integer lands on the grid."""
+    lv = torch.tensor(list(levels), dtype=torch.int32)
+    basis = torch.cumprod(torch.tensor([1] + list(levels[:-1])), dim=0, dtype=torch.int32)
+    level_idx = (indices[..., None] // basis) % lv
+    half_width = lv // 2
+    codes = (level_idx - half_width) / half_width  # _scale_and_shift_inverse (:155-157)
+    if (prefix + "project_out.weight") in sd:
+        codes = F.linear(codes, sd[prefix + "project_out.weight"], sd[prefix + "project_out.bias"])
+    return codes.transpose(1, 2)
+
+
 def strip_prefix(sd: Mapping[str, Tensor], prefix: str) -> Dict[str, Tensor]:
     return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
 

@@ -232,6 +232,8 @@ def test_torch_ops_registered_with_schemas_and_fakes():
     assert ns.vq2emb_ct(m(2, 12, 3, dt=torch.int64), m(3, 8192, 8), m(3, 1024, 8), m(3, 1024)).shape == (2, 1024, 12)
     post, idx = ns.fsq(m(2, 512, 9), w, w, w, w, w)
     assert post.shape == (2, 512, 9) and idx.dtype == torch.int32
+    tok = ns.fsq_codes(m(2, 9, dt=torch.int32), m(512, 4), m(512), [4, 4, 4, 8])
+    assert tok.shape == (2, 512, 9) and tok.dtype == torch.float32
     assert ns.resample_sinc(m(3, 160), w, 240, 256, 2, 3, 16, 6).shape == (3, 256)
 
 

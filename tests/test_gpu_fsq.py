@@ -68,3 +68,46 @@ def test_fsq_identity_projection_and_all_codes(dev):
     assert torch.equal(q.cpu(), ref_q)
     assert len(torch.unique(q)) == int(np.prod(levels))
     assert torch.equal(post.cpu(), ref_post)
+
+
+@pytest.mark.parametrize("fname", FSQ_FILES)
+def test_fsq_tokens_to_audio_against_reference(dev, golden, fname, tmp_path):
+    """The fsq=True decoder's token -> audio path (FSQ.indices_to_codes, finite_scalar_quantization.py:176-192,
+    on bc_fsq_codes; the reference decoder's vq2emb has no FSQ branch and raises AttributeError, as ours does):
+      * indices_to_codes of the reference's indices (int32 as forward returns them, and int64 as the token files
+        give them) equals this path's own forward post bit for bit and the reference's within 1e-6 of max|ref|
+        (project_out: 4-term fma chain vs MKL);
+      * out-of-range and negative integers wrap exactly as torch's floor // and % wrap them (reference fixture);
+      * tokens -> .npy files -> decode_index_files -> waveform within the decoder bound of the reference's
+        waveform (MSE <= 1e-12, max|d| <= 1e-5)."""
+    from audiotokenization_amd.extract import save_indices
+    from audiotokenization_amd.tokens import decode_index_files
+
+    g = golden(fname)
+    meta = g["meta"]
+    _, dec, *_ = build_models(meta["model"], device=dev, **meta["overrides"])
+    codes = torch.from_numpy(g["codes"])  # (B, F) int32, the reference's indices
+    with torch.no_grad():
+        post, q, _ = dec(torch.from_numpy(g["z"]).to(dev), vq=True)
+        t32 = dec.quantizer.indices_to_codes(codes.to(dev))
+        t64 = dec.quantizer.indices_to_codes(codes.long().to(dev))
+        wrap = dec.quantizer.indices_to_codes(torch.from_numpy(g["wrap_idx"]).to(dev))
+        wrap32 = dec.quantizer.indices_to_codes(torch.from_numpy(g["wrap_idx"]).int().to(dev))
+        torch.cuda.synchronize()
+    with pytest.raises(AttributeError):
+        dec.vq2emb(codes[:, :, None].long().to(dev))
+    assert t32.shape == g["tok_post"].shape and torch.equal(t32, t64) and torch.equal(wrap, wrap32)
+    same = (q.cpu() == codes).all()
+    if bool(same):
+        assert torch.equal(t32, post), "indices_to_codes(forward's indices) != forward's post"
+    assert_close_rel(t32.cpu(), torch.from_numpy(g["tok_post"]), 1e-6, "fsq indices_to_codes")
+    assert_close_rel(wrap.cpu(), torch.from_numpy(g["wrap_post"]), 1e-6, "fsq indices_to_codes (wrapped)")
+    paths = [save_indices(str(tmp_path), "fsq", f"1_1_000001_{i:06d}", g["codes"][i][:, None].astype(np.int16))
+             for i in range(codes.shape[0])]
+    wavs = decode_index_files(dec, paths, dev)
+    for i, w in enumerate(wavs):
+        r = g["wav"][i, 0].astype(np.float64)
+        d = w.astype(np.float64) - r
+        mse, mx = float((d ** 2).mean()), float(np.abs(d).max())
+        print(f"{fname} clip {i}: tokens -> audio mse {mse:.2e} max {mx:.2e}")
+        assert w.shape == r.shape and mse <= 1e-12 and mx <= 1e-5, (mse, mx)

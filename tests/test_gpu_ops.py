@@ -66,6 +66,10 @@ def _cases(dev, base):
     cases.append(("vq2emb", (idx, 0, cb, w_out, b_out)))
     cst, wst, bst = dec.quantizer.prepared_stack(dev)
     cases.append(("vq2emb_ct", (idx, cst, wst, bst)))
+    fq = M.FSQ([4, 4, 4, 8], dim=64, channel_first=True).eval()
+    fw_in, fb_in, fw_out, fb_out, fconsts = fq.prepared(dev)
+    cases.append(("fsq", (torch.randn(2, 64, 13, generator=g).to(dev), fw_in, fb_in, fw_out, fb_out, fconsts)))
+    cases.append(("fsq_codes", (torch.randint(-600, 1200, (2, 13), generator=g).to(dev), fw_out, fb_out, fq.levels)))
     return cases
 
 
@@ -77,7 +81,7 @@ def test_opcheck_every_codec_op(dev, base):
     for name, args in _cases(dev, base):
         torch.library.opcheck(getattr(ns, name).default, args)
         seen.add(name)
-    assert {"conv1d", "snake", "tanh", "reslstm", "reslstm_bidir", "vq", "vq2emb", "vq2emb_ct"} <= seen
+    assert {"conv1d", "snake", "tanh", "reslstm", "reslstm_bidir", "vq", "vq2emb", "vq2emb_ct", "fsq", "fsq_codes"} <= seen
 
 
 def test_ops_equal_the_raw_c_abi(dev, base):

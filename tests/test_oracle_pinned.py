@@ -135,6 +135,11 @@ def test_fsq_fixture(golden, fname):
     assert idx.dtype == torch.int32 and torch.equal(idx, torch.from_numpy(g["codes"]))
     assert torch.equal(post, torch.from_numpy(g["post"]))
     assert torch.equal(wav, torch.from_numpy(g["wav"]))
+    # token -> latent: indices_to_codes of the reference's own indices and of wrapped / negative integers
+    tok = O.fsq_indices_to_codes(torch.from_numpy(g["codes"]), sd, meta["levels"])
+    assert torch.equal(tok, torch.from_numpy(g["tok_post"]))
+    wrap = O.fsq_indices_to_codes(torch.from_numpy(g["wrap_idx"]), sd, meta["levels"])
+    assert torch.equal(wrap, torch.from_numpy(g["wrap_post"]))
 
 
 @pytest.mark.parametrize("nq", [2, 4])

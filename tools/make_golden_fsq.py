@@ -5,8 +5,8 @@ Run in the development container only (the reference never travels):
     python tools/make_golden_fsq.py
 Fixture = data: the latents fed to the quantizer (the reference debug / base encoder's output on synthetic
 clips, scaled to exercise every level), the reference's quantized output, its indices, the fp64 distance
-of every bounded coordinate to its nearest rounding boundary (the certificate for an index flip), and the
-decoded waveform.  Weights are not stored: both sides synthesise them (synth.synth_state_dict).
+of every bounded coordinate to its nearest rounding boundary (the certificate for an index flip), the
+decoded waveform, and the FSQ's indices_to_codes of its own indices and of out-of-range / negative integers.  Weights are not stored: both sides synthesise them (synth.synth_state_dict).
 """
 from __future__ import annotations
 
@@ -50,8 +50,17 @@ def fsq_case(ref, name, n_clips, n_samples, levels, gain, random_frames=0):
     bounded = (zi + shift).tanh() * half_l - offset
     margin = ((bounded - bounded.floor()) - 0.5).abs().amin(dim=-1)  # distance to the nearest .5 boundary
     wav = dec(post, vq=False)
+    # token -> latent (finite_scalar_quantization.py:176-192; the decoder's own vq2emb has no FSQ branch):
+    # the reference's indices_to_codes of its own indices, and of integers outside [0, codebook_size) and
+    # negative ones (torch's floor // and % wrap them onto the grid)
+    tok_post = fsq.indices_to_codes(q)
+    g = torch.Generator().manual_seed(11)
+    wrap_idx = torch.cat([torch.randint(-3 * cb, 4 * cb, (q.shape[0], 29), generator=g),
+                          torch.tensor([[-1, cb, cb - 1, -cb, 2 * cb + 1, 0, -(cb + 1)]] * q.shape[0])], dim=1)
+    wrap_post = fsq.indices_to_codes(wrap_idx)
     out = dict(z=z.numpy(), post=post.numpy(), codes=q.numpy().astype(np.int32), margin=margin.float().numpy(),
-               wav=wav.numpy(), loss=loss.numpy())
+               wav=wav.numpy(), loss=loss.numpy(), tok_post=tok_post.numpy(), wrap_idx=wrap_idx.numpy(),
+               wrap_post=wrap_post.numpy())
     meta = dict(model=name, overrides=dict(fsq=True, fsq_levels=list(levels), codebook_size=cb), gain=gain,
                 torch=torch.__version__, levels=list(levels))
     tag = f"fsq_{name}_" + "x".join(map(str, levels)) + ("_rand" if random_frames else "")
