@@ -58,6 +58,7 @@ _SIGS = {
     "bc_vq2emb_ct": (I, [P, I, P, P, P, P, I, I, I, I, I, P]),
     "bc_fsq_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, P]),
     "bc_fsq_codes": (I, [P, I, P, P, P, P, I, I, I, I, P]),
+    "bc_stream_window": (I, [P, L, L, P, P, P, P, P, I, I, I, I, P]),
     "bc_resample_sinc": (I, [P, P, P, I, L, L, L, I, I, I, I, P]),
     "bc_rvq_update": (I, [P, P, P, L, I, P]),
     "bc_btc_to_ctb": (I, [P, P, I, I, I, P]),
@@ -72,7 +73,7 @@ _SIGS = {
     "bc_debug_selftest": (I, [I, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 13  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 14  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

@@ -494,6 +494,13 @@ int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float
   return fsq_fwd_launch(z, w_in, b_in, w_out, b_out, consts, idx, post, B, D, T, d, S(stream));
 }
 
+int bc_stream_window(const float* x, long long x_batch_stride, long long x_row_stride, const float* ctx,
+                     const float* snake_alpha_exp, const float* snake_inv_beta, float* win, float* ctx_out, int B, int C,
+                     int n, int P, void* stream) {
+  return stream_window_launch(x, x_batch_stride, x_row_stride, ctx, snake_alpha_exp, snake_inv_beta, win, ctx_out, B, C,
+                              n, P, S(stream));
+}
+
 int bc_fsq_codes(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
                  float* post, int B, int D, int T, int d, void* stream) {
   return fsq_codes_launch(idx, idx_bits, levels, w_out, b_out, post, B, D, T, d, S(stream));

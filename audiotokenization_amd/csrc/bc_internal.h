@@ -75,6 +75,8 @@ int resunit_rr_launch(const float* x_raw, const float* x_act, const float* w7, c
 
 int snake_launch(const float* x, const float* sa, const float* sb, float* y, int B, int C,
                  long long T, hipStream_t st);
+int stream_window_launch(const float* x, long long xbs, long long xT, const float* ctx, const float* sa, const float* sb,
+                         float* win, float* ctx_out, int B, int C, int n, int P, hipStream_t st);
 int aa_snake_launch(const float* x, const float* sa, const float* sb, const float* fu,
                     const float* fd, float* y, int B, int C, int T, hipStream_t st);
 int btc_to_ctb_launch(const float* x, float* y, int B, int C, int T, hipStream_t st);

@@ -10,6 +10,7 @@
 //                     the 2T intermediate never leaves LDS.
 //  transpose kernels: [B][C][T] <-> [C][T][B] layouts around the ResLSTM (vq/module.py:160-166).
 //  synth_clips      : counter-hash white noise generated in HBM.
+//  stream_window    : a causal stream's [carried context | chunk] window (+ Snake) and its next context.
 #include "bc_common.h"
 #include "bc_internal.h"
 
@@ -181,6 +182,49 @@ int snake_launch(const float* x, const float* sa, const float* sb, float* y, int
   if (total == 0) return BC_OK;
   hipLaunchKernelGGL(snake_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, sa, sb, y, C, T,
                      total);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
+}
+
+// Streaming context window (streaming.py, causal streaming encode / decode): for each (b, c) row
+//   win[j]     = j < P ? ctx[j] : act(x[j - P])   (j < P + n: the [carried context | chunk] input of a causal conv,
+//                                                  or of a whole one-launch ResidualUnit)
+//   ctx_out[i] = win[n + i]                        (i < P: the context the next chunk carries)
+// in one pass.  act = SnakeBeta through snake() (bit-identical to snake_kernel's pairs and to the convs' Snake
+// epilogue) or the identity; a missing ctx reads zeros (a stream's first chunk: the causal conv's zero padding,
+// and snake(0) = 0, so zeros are the same before and after the activation).  x may be a strided view (row pitch
+// xT, batch pitch xbs): a ResidualUnit run over its own window hands its last n columns on without a copy.
+__global__ void __launch_bounds__(256) stream_window_kernel(const float* __restrict__ x, long long xbs, long long xT,
+                                                            const float* __restrict__ ctx, const float* __restrict__ sa,
+                                                            const float* __restrict__ sb, float* __restrict__ win,
+                                                            float* __restrict__ ctx_out, int C, int n, int P,
+                                                            long long total) {
+  const long long W = (long long)P + n;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long row = i / W, j = i - row * W;
+    const int c = (int)(row % C);
+    const long long b = row / C;
+    float v;
+    if (j < P) {
+      v = ctx ? ctx[row * P + j] : 0.f;
+    } else {
+      v = x[b * xbs + c * xT + (j - P)];
+      if (sa) v = snake(v, sa[c], sb[c]);
+    }
+    win[i] = v;
+    if (j >= n) ctx_out[row * P + (j - n)] = v;
+  }
+}
+
+int stream_window_launch(const float* x, long long xbs, long long xT, const float* ctx, const float* sa, const float* sb,
+                         float* win, float* ctx_out, int B, int C, int n, int P, hipStream_t st) {
+  if (!x || !win || B < 0 || C < 1 || n < 1 || P < 0 || xT < n || xbs < (long long)(C - 1) * xT + n) return BC_ERR_ARG;
+  if ((sa == nullptr) != (sb == nullptr) || (P > 0 && !ctx_out)) return BC_ERR_ARG;
+  const long long total = (long long)B * C * ((long long)P + n);
+  if (total == 0) return BC_OK;
+  hipLaunchKernelGGL(stream_window_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, xbs, xT, ctx, sa, sb, win,
+                     ctx_out, C, n, P, total);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

@@ -385,6 +385,24 @@ Tensor vq2emb_ct(const Tensor& idx, const Tensor& cbs, const Tensor& w_out, cons
   return out;
 }
 
+std::vector<Tensor> stream_window(const Tensor& x, const optional<Tensor>& ctx, const optional<Tensor>& a,
+                                  const optional<Tensor>& ib, int64_t P) {
+  TORCH_CHECK(x.is_cuda(), "bigcodec: x must be a HIP device tensor (there is no CPU path)");
+  TORCH_CHECK_VALUE(x.scalar_type() == at::kFloat && x.dim() == 3 && x.stride(2) == 1,
+                    "bigcodec::stream_window: x must be a (B, C, n) float32 tensor with unit time stride");
+  const int64_t B = x.size(0), C = x.size(1), n = x.size(2);
+  TORCH_CHECK_VALUE(P >= 0 && n >= 1, "bigcodec::stream_window: P >= 0 and a non-empty chunk");
+  check_coeffs(a, ib, C, "stream_window");
+  if (ctx) TORCH_CHECK_VALUE(ctx->sizes() == at::IntArrayRef({B, C, P}), "bigcodec::stream_window: ctx must be (B, C, P)");
+  auto win = at::empty({B, C, P + n}, x.options());
+  auto nctx = at::empty({B, C, P}, x.options());
+  ok(bc_stream_window(x.data_ptr<float>(), B > 1 ? x.stride(0) : C * x.stride(1), C > 1 ? x.stride(1) : n,
+                      optf(x, ctx, "ctx"), optf(x, a, "alpha_exp"), optf(x, ib, "inv_beta"), win.data_ptr<float>(),
+                      nctx.data_ptr<float>(), i32(B, "B"), i32(C, "C"), i32(n, "n"), i32(P, "P"), stream_of(x)),
+     "bc_stream_window");
+  return {win, nctx};
+}
+
 Tensor fsq_codes(const Tensor& idx, const Tensor& w_out, const Tensor& b_out, at::IntArrayRef levels) {
   TORCH_CHECK_VALUE(idx.is_cuda() && (idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong) &&
                         idx.is_contiguous(),
@@ -482,6 +500,7 @@ TORCH_LIBRARY(bigcodec, m) {
   m.def("vq2emb_ct(Tensor idx, Tensor codebooks, Tensor w_out, Tensor b_out) -> Tensor");
   m.def("fsq(Tensor z, Tensor w_in, Tensor b_in, Tensor w_out, Tensor b_out, Tensor consts) -> Tensor[]");
   m.def("fsq_codes(Tensor idx, Tensor w_out, Tensor b_out, int[] levels) -> Tensor");
+  m.def("stream_window(Tensor x, Tensor? ctx, Tensor? alpha_exp, Tensor? inv_beta, int P) -> Tensor[]");
   m.def("resample_sinc(Tensor x, Tensor kern, int lout, int pitch, int orig, int new_freq, int taps, int width) -> Tensor");
   m.def("synth_clips_(Tensor(a!) x, int clip0) -> ()");
 }
@@ -505,6 +524,7 @@ TORCH_LIBRARY_IMPL(bigcodec, CUDA, m) {
   m.impl("vq2emb_ct", &Guarded<&vq2emb_ct>::call);
   m.impl("fsq", &Guarded<&fsq>::call);
   m.impl("fsq_codes", &Guarded<&fsq_codes>::call);
+  m.impl("stream_window", &Guarded<&stream_window>::call);
   m.impl("resample_sinc", &Guarded<&resample_sinc>::call);
   m.impl("synth_clips_", &Guarded<&synth_clips_>::call);
 }

@@ -25,7 +25,7 @@ _ns = None
 
 # every op the extension defines (tests check the registry against this list)
 OPS = ("conv1d", "conv_transpose1d", "resunit", "snake", "aa_snake", "aa_snake_ex", "tanh", "reslstm", "reslstm_bidir", "vq_prepare_codebook", "vq",
-       "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "fsq_codes", "resample_sinc", "synth_clips_")
+       "vq_argmin", "vq2emb", "vq2emb_add_", "rvq_update_", "vq2emb_ct", "fsq", "fsq_codes", "stream_window", "resample_sinc", "synth_clips_")
 
 
 def load():
@@ -144,6 +144,11 @@ def _register_fakes():
     def _fsq_codes(idx, w_out, b_out, levels):
         B, T = idx.shape
         return _new(idx, (B, b_out.shape[0], T), torch.float32)
+
+    @reg("bigcodec::stream_window")
+    def _stream_window(x, ctx, a, ib, P):
+        B, C, n = x.shape
+        return [_new(x, (B, C, P + n)), _new(x, (B, C, P))]
 
     @reg("bigcodec::resample_sinc")
     def _resample(x, kern, lout, pitch, orig, new_freq, taps, width):

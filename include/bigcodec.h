@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 13
+#define BC_ABI_VERSION 14
 
 int bc_abi_version(void);
 
@@ -259,6 +259,17 @@ int bc_fsq_fwd(const float* z, const float* w_in, const float* b_in, const float
  *   for the indices it returned.  1 <= d <= 8. */
 int bc_fsq_codes(const void* idx, int idx_bits, const int* levels, const float* w_out, const float* b_out,
                  float* post, int B, int D, int T, int d, void* stream);
+
+/* bc_stream_window: one step of a causal stream's carried state (audiotokenization_amd/streaming.py; the reference has
+ *   no streaming mode, its whole-sequence causal convs, vq/module.py:11-48, define the result): for each row (b, c)
+ *   win[b][c][j] = j < P ? ctx[b][c][j] : act(x[b][c][j - P]) for j < P + n, and ctx_out[b][c][i] = win[b][c][n + i]
+ *   for i < P.  act = SnakeBeta with (snake_alpha_exp, snake_inv_beta) as bc_snake_fwd takes them, or the identity
+ *   when both are NULL; ctx NULL reads zeros (a stream's start).  x is read at x + b * x_batch_stride + c *
+ *   x_row_stride + t (floats), so a strided view works; win is [B][C][P + n], ctx / ctx_out [B][C][P] (ctx_out may be
+ *   NULL only when P == 0) and must not overlap ctx. */
+int bc_stream_window(const float* x, long long x_batch_stride, long long x_row_stride, const float* ctx,
+                     const float* snake_alpha_exp, const float* snake_inv_beta, float* win, float* ctx_out, int B, int C,
+                     int n, int P, void* stream);
 
 /* ---- Real-audio ingest ------------------------------------------------------------------------
  * bc_resample_sinc: torchaudio.transforms.Resample(orig, new) as extract_indices.py:129-132 and

@@ -234,6 +234,8 @@ def test_torch_ops_registered_with_schemas_and_fakes():
     assert post.shape == (2, 512, 9) and idx.dtype == torch.int32
     tok = ns.fsq_codes(m(2, 9, dt=torch.int32), m(512, 4), m(512), [4, 4, 4, 8])
     assert tok.shape == (2, 512, 9) and tok.dtype == torch.float32
+    win, nctx = ns.stream_window(m(2, 48, 100), m(2, 48, 18), m(48), m(48), 18)
+    assert win.shape == (2, 48, 118) and nctx.shape == (2, 48, 18)
     assert ns.resample_sinc(m(3, 160), w, 240, 256, 2, 3, 16, 6).shape == (3, 256)
 
 

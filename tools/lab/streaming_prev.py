@@ -13,13 +13,8 @@ concatenation of the chunks' latents equals the encoder's output on the concaten
 bit in the exact-split x6 precision; in h3 the per-tile block scales differ between the two tilings, so
 the outputs agree to fp32 rounding).  Chunks must be a multiple of the hop (prod(up_ratios)) samples.
 Anti-aliased activations are not causal (act.py / resample.py look ahead), so antialias=True is refused.
-The carried contexts live on the device and every step of the state is one bc_stream_window launch: it writes the
-[context | chunk] window (with the stage's Snake applied on the way) and the next context in one pass.  A
-ResidualUnit the one-launch kernel serves (bc_resunit_fwd_snake_in: C = 48 / 96 in h3, x6, bf16) runs as ONE
-launch over its raw window with its own causal padding: output column P + t sees window columns t … P + t, all
-real samples, and its residual is the window's own column P + t; the first P = 6d outputs are dropped by taking the
-view [P:] (no copy: the next window reads the strided view).  Other units run conv7 (Snake epilogue) and conv1
-(residual add) over their activated window.  No torch compute kernel runs in a push.
+Inside a chunk the ResidualUnits run as two conv launches (the one-launch kernel keeps input and output
+lengths equal), and the carried contexts are prepended with torch.cat on the device.
 
 StreamingDecoder is the same for a causal BigCodecDecoder (vq/codec_decoder.py:15-94 with causal=True): latent
 frames in, waveform out.  Its upsamplers are CausalConvTranspose1d (vq/module.py:50-57: ConvTranspose1d with
@@ -33,11 +28,11 @@ from typing import Dict, Optional
 
 import torch
 
-from . import _lib
-from . import ops
-from .blocks import DecoderBlock, EncoderBlock, ResLSTM, _conv_of
-from .conv import CausalConvTranspose1d, ConvTranspose1dWN
-from .modules import _as_input
+from audiotokenization_amd import _lib
+from audiotokenization_amd import ops
+from audiotokenization_amd.blocks import DecoderBlock, EncoderBlock, ResLSTM, _conv_of
+from audiotokenization_amd.conv import CausalConvTranspose1d, ConvTranspose1dWN
+from audiotokenization_amd.modules import _as_input
 
 
 class StreamingEncoder:
@@ -61,38 +56,17 @@ class StreamingEncoder:
         self._lstm: Dict[int, tuple] = {}
         self.samples = 0
 
-    def _window(self, key, x, P: int, act=None):
-        """[carried context | x] (B, C, P + n), `act` (a Snake Activation1d or None) applied to x, as the input of a
-        stage with P columns of causal history; the last P columns become the next chunk's context."""
-        sa, sb = act.act.coeffs(x.device) if act is not None else (None, None)
-        win, nctx = ops.load().stream_window(x, self._ctx.get(key) if P else None, sa, sb, P)
-        if P:
-            self._ctx[key] = nctx
-        return win
-
-    def _conv(self, wrapper, x, act=None, residual=None, out_snake=None, epilogue: int = 0):
-        """A causal conv over [context | act(x)] with no padding: exactly the chunk's outputs."""
+    def _conv(self, wrapper, xa, residual=None):
         c = _conv_of(wrapper)
         P = c.pad_left()
-        if P == 0 and act is None and x.is_contiguous():
-            return c.run(x, residual, epilogue, out_snake)
-        return c.run(self._window(id(c), x, P, act), residual, epilogue, out_snake, pad_left=0)
-
-    def _dense(self, h):
-        """A contiguous copy of a strided chunk view (one launch), for the ops that take dense tensors."""
-        return h if h.is_contiguous() else self._window(None, h, 0)
-
-    def _unit(self, ru, h):
-        """One ResidualUnit on a chunk: x + conv1(act2(conv7(act1(x)))) (vq/module.py:74-89)."""
-        cfg = ru._fused_cfg()
-        conv7 = _conv_of(ru.block[1])
-        if cfg >= 0 and ru.snake_on_load():
-            P = conv7.pad_left()  # 6d: the unit's whole history
-            win = self._window(("ru", id(ru)), h, P)
-            y = ru._flow_fused(cfg, win, None, True, None)[0]
-            return y[:, :, P:]
-        t = self._conv(ru.block[1], h, act=ru.block[0], out_snake=ru.block[2].act.coeffs(h.device))
-        return self._conv(ru.block[3], t, residual=self._dense(h))
+        if P == 0:
+            return c.run(xa, residual)
+        ctx = self._ctx.get(id(c))
+        if ctx is None:
+            ctx = torch.zeros((xa.shape[0], xa.shape[1], P), device=xa.device, dtype=torch.float32)
+        xin = torch.cat([ctx, xa], dim=2)
+        self._ctx[id(c)] = xin[:, :, -P:].contiguous()
+        return c.run(xin, residual, pad_left=0)
 
     def _lstm_run(self, m: ResLSTM, h):
         y, state = m.run(h, state=self._lstm.get(id(m)), return_state=True)
@@ -113,15 +87,16 @@ class StreamingEncoder:
         for st in blk[1:-2]:
             if isinstance(st, EncoderBlock):
                 sub = list(st.block)
-                for ru in sub[:-2]:
-                    h = self._unit(ru, h)
-                h = self._conv(sub[-1], h, act=sub[-2])
+                for ru in sub[:-2]:  # ResidualUnit: x + conv1(act2(conv7(act1(x))))
+                    t = self._conv(ru.block[1], ru.block[0](h))
+                    h = self._conv(ru.block[3], ru.block[2](t), residual=h)
+                h = self._conv(sub[-1], sub[-2](h))
             elif isinstance(st, ResLSTM):
                 h = self._lstm_run(st, h)
             else:
                 raise NotImplementedError(f"unexpected encoder stage {type(st).__name__}")
         self.samples += x.shape[-1]
-        out = self._conv(last_conv, h, act=final_act)
+        out = self._conv(last_conv, final_act(h))
         _lib.check_status()
         return out
 
@@ -151,16 +126,23 @@ class StreamingDecoder(StreamingEncoder):
         self.hop = int(decoder.hop_length)
         self.reset()
 
-    def _convT(self, wrapper, h, act):
+    def _convT(self, wrapper, xa, out_snake=None):
         conv = wrapper.conv if isinstance(wrapper, CausalConvTranspose1d) else wrapper
         s, K = conv.stride, conv.kernel_size
         if K % s:
             raise NotImplementedError(f"streaming transposed conv needs kernel_size % stride == 0 (k={K}, s={s})")
         c = K // s - 1  # input frames of history an output block needs
-        x = self._window(id(conv), h, c, act)
+        x = xa
+        if c:
+            ctx = self._ctx.get(id(conv))
+            if ctx is None:
+                ctx = torch.zeros((xa.shape[0], xa.shape[1], c), device=xa.device, dtype=torch.float32)
+            x = torch.cat([ctx, xa], dim=2)
+            self._ctx[id(conv)] = x[:, :, -c:].contiguous()
         phases, _, bias, cfg = conv.prepared(x.device)
+        sa, sb = out_snake if out_snake is not None else (None, None)
         # full length (n + c - 1) s + K; padding c * s crops c * s on both sides: the n * s outputs of this chunk
-        out = ops.load().conv_transpose1d(x, phases, bias, None, None, conv.out_channels, h.shape[-1] * s, K, s, c * s,
+        out = ops.load().conv_transpose1d(x, phases, bias, sa, sb, conv.out_channels, xa.shape[-1] * s, K, s, c * s,
                                           cfg, False)
         return out[0]
 
@@ -182,15 +164,27 @@ class StreamingDecoder(StreamingEncoder):
                 h = self._lstm_run(st, h)
             elif isinstance(st, DecoderBlock):
                 sub = list(st.block)
-                h = self._convT(sub[1], h, sub[0])
-                for ru in sub[2:]:
-                    h = self._unit(ru, h)
+                h = self._convT(sub[1], sub[0](h))
+                for ru in sub[2:]:  # ResidualUnit: x + conv1(act2(conv7(act1(x))))
+                    t = self._conv(ru.block[1], ru.block[0](h))
+                    h = self._conv(ru.block[3], ru.block[2](t), residual=h)
             else:
                 raise NotImplementedError(f"unexpected decoder stage {type(st).__name__}")
         self.samples += z.shape[-1] * self.hop
-        out = self._conv(last_conv, h, act=final_act, epilogue=1)  # the decoder's nn.Tanh in the epilogue
+        out = self._conv_tanh(last_conv, final_act(h))
         _lib.check_status()
         return out
+
+    def _conv_tanh(self, wrapper, xa):
+        """The last conv with the decoder's nn.Tanh fused in its epilogue (codec_decoder.py:80)."""
+        c = _conv_of(wrapper)
+        P = c.pad_left()
+        ctx = self._ctx.get(id(c))
+        if ctx is None:
+            ctx = torch.zeros((xa.shape[0], xa.shape[1], P), device=xa.device, dtype=torch.float32)
+        xin = torch.cat([ctx, xa], dim=2)
+        self._ctx[id(c)] = xin[:, :, -P:].contiguous()
+        return c.run(xin, None, 1, pad_left=0)
 
     def decode(self, z, chunk: int) -> torch.Tensor:
         """Whole latent sequence through `push` in chunks of `chunk` frames (the last may be shorter)."""
