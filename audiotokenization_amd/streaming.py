@@ -125,6 +125,10 @@ class StreamingEncoder:
         _lib.check_status()
         return out
 
+    def graph(self, example) -> "StreamGraph":
+        """This stream's push for chunks shaped like `example`, captured once in a HIP graph (StreamGraph)."""
+        return StreamGraph(self, example)
+
     def encode(self, x, chunk: int) -> torch.Tensor:
         """Whole input through `push` in chunks of `chunk` samples (the last may be shorter)."""
         self.reset()
@@ -197,3 +201,70 @@ class StreamingDecoder(StreamingEncoder):
         self.reset()
         outs = [self.push(z[..., i:i + chunk]) for i in range(0, z.shape[-1], chunk)]
         return torch.cat(outs, dim=2)
+
+
+class StreamGraph:
+    """One push of a fixed chunk shape captured in a HIP graph (torch.cuda.CUDAGraph: hipStreamBeginCapture /
+    hipGraphLaunch on ROCm) and replayed per chunk: the dozens of launches of a push (a window, a conv or a
+    one-launch ResidualUnit per stage, the persistent ResLSTM) go to the device as ONE graph launch, so a stream
+    of short chunks is no longer bound by host-side dispatch.  The carried state lives in static buffers: the
+    graph reads them, its stages write the next state into graph-owned tensors, and the graph's last nodes copy
+    those back into the static buffers.  The stream's current state is taken over at capture (the warm-up push
+    that sizes every buffer is undone), and the stream continues from the graph's state afterwards.
+
+    push(x) copies x into the static input, replays, and returns the graph's static output (overwritten by the next
+    push: copy it to keep it).  check=True (the default) reads the ResLSTM status words after the replay (one
+    host wait, as StreamingEncoder.push does); check=False skips it and check() reads them later.  The
+    results equal the eager stream's bit for bit (tests/test_gpu_streaming.py)."""
+
+    def __init__(self, stream: StreamingEncoder, example):
+        example = _as_input(example)
+        self.stream = stream
+        self.input = example.clone()
+        # one eager push sizes every carried state and warms the weight caches; then the state before it returns
+        ctx0 = {k: v.clone() for k, v in stream._ctx.items()}
+        lstm0 = {k: tuple(t.clone() for t in v) for k, v in stream._lstm.items()}
+        samples0 = stream.samples
+        with torch.no_grad():
+            stream.push(self.input)
+        self._ctx = {k: (ctx0[k] if k in ctx0 else torch.zeros_like(v)) for k, v in stream._ctx.items()}
+        self._lstm = {k: (lstm0[k] if k in lstm0 else tuple(torch.zeros_like(t) for t in v))
+                      for k, v in stream._lstm.items()}
+        stream._ctx, stream._lstm, stream.samples = dict(self._ctx), dict(self._lstm), samples0
+        torch.cuda.synchronize()
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), _lib.deferred_status() as ticket:
+            with torch.cuda.graph(self._graph):
+                self.output = stream.push(self.input)
+                for k, v in stream._ctx.items():
+                    self._ctx[k].copy_(v)
+                for k, v in stream._lstm.items():
+                    for dst, src in zip(self._lstm[k], v):
+                        dst.copy_(src)
+        self._status = ticket.items  # the graph's own status words, rewritten by every replay
+        stream._ctx, stream._lstm, stream.samples = dict(self._ctx), dict(self._lstm), samples0
+        self._n = example.shape[-1] * (stream.hop if isinstance(stream, StreamingDecoder) else 1)
+
+    def push(self, x, check: bool = True) -> torch.Tensor:
+        if tuple(x.shape) != tuple(self.input.shape):
+            raise ValueError(f"this graph was captured for chunks of shape {tuple(self.input.shape)}, got {tuple(x.shape)}")
+        self.input.copy_(x)
+        self._graph.replay()
+        self.stream.samples += self._n
+        if check:
+            self.check()
+        return self.output
+
+    def reset(self) -> None:
+        """Start a new stream on this graph: the static state back to zeros (a fresh stream's context)."""
+        for v in self._ctx.values():
+            v.zero_()
+        for v in self._lstm.values():
+            for t in v:
+                t.zero_()
+        self.stream._ctx, self.stream._lstm, self.stream.samples = dict(self._ctx), dict(self._lstm), 0
+
+    def check(self) -> None:
+        """Raise BigCodecLibraryError if the last replay's persistent ResLSTM reported a failure (host wait)."""
+        if self._status:
+            _lib._raise_bad(self._status, torch.cat([t.reshape(-1) for t, _ in self._status]).cpu().tolist())

@@ -139,3 +139,44 @@ def test_stream_window_kernel(dev, P, n, strided, act, first):
     ref = torch.cat([ctx if ctx is not None else torch.zeros(B, C, P, device=dev), xa], dim=2)
     assert torch.equal(win, ref)
     assert nctx.shape == (B, C, P) and torch.equal(nctx, ref[:, :, ref.shape[2] - P:])
+
+
+@pytest.mark.parametrize("sprec", ["h3", "x6"])
+def test_stream_graph_equals_eager_stream(dev, sprec):
+    """StreamGraph (one HIP-graph replay per chunk): the encode and decode streams equal the eager streams bit for
+    bit, when captured on a fresh stream and when captured mid-stream (the graph takes the eager stream's carried
+    context and ResLSTM state over); a chunk of another shape is refused; the ResLSTM status words are read."""
+    from audiotokenization_amd.streaming import StreamingDecoder
+
+    old = L.precision_mode()
+    try:
+        L.set_precision(sprec)
+        enc, dec, *_ = build_models("default", device=dev, causal=True)
+        B, n, ch = 2, 6000, 1200
+        x = torch.from_numpy(synth.synth_clips(B, n, clip0=31)).unsqueeze(1).to(dev)
+        with torch.no_grad():
+            eager = StreamingEncoder(enc).encode(x, ch)
+            s = StreamingEncoder(enc)
+            g = s.graph(x[..., :ch])
+            fresh = torch.cat([g.push(x[..., i:i + ch]).clone() for i in range(0, n, ch)], dim=2)
+            s2 = StreamingEncoder(enc)
+            first = s2.push(x[..., :ch])  # eager, then the graph continues the same stream
+            g2 = s2.graph(x[..., :ch])
+            mid = torch.cat([first] + [g2.push(x[..., i:i + ch]).clone() for i in range(ch, n, ch)], dim=2)
+            with pytest.raises(ValueError):
+                g2.push(x[..., :ch // 2])
+            post = dec(eager, vq=True)[0]
+            fc = 6
+            d_eager = StreamingDecoder(dec).decode(post, fc)
+            sd = StreamingDecoder(dec)
+            gd = sd.graph(post[..., :fc])
+            d_graph = torch.cat([gd.push(post[..., i:i + fc]).clone() for i in range(0, post.shape[-1], fc)], dim=2)
+            torch.cuda.synchronize()
+        assert torch.equal(fresh, eager), f"graph stream != eager stream: {max_rel_err(fresh, eager):.3e}"
+        assert torch.equal(mid, eager), f"mid-stream graph != eager stream: {max_rel_err(mid, eager):.3e}"
+        assert torch.equal(d_graph, d_eager), f"graph decode stream != eager: {max_rel_err(d_graph, d_eager):.3e}"
+        assert s.samples == n and sd.samples == post.shape[-1] * dec.hop_length
+        assert g._status, "the graph holds the ResLSTM status words"
+        g.check()
+    finally:
+        L._mode = old

@@ -4,6 +4,7 @@
 
 Prints audio-seconds per second of the stream (every chunk of a B-clip batch pushed back to back, HIP-synchronised
 around the whole stream), ms per push and the number of kernel launches per push (rocprofv3 gives the names).
+--graph replays one captured HIP graph per chunk (StreamGraph; status words read once at the end).
 --prev times the round-4 first-session stream (tools/lab/streaming_prev.py: separate Snake launches, torch.cat
 contexts, two-launch ResidualUnits) on the same models for an A/B.  Random weights, synthetic white noise.
 """
@@ -42,6 +43,7 @@ def main():
     p.add_argument("--prev", action="store_true")
     p.add_argument("--decode", action="store_true")
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--graph", action="store_true", help="push through a StreamGraph (one HIP-graph replay per chunk)")
     a = p.parse_args()
     if a.prev:
         import streaming_prev as S
@@ -61,19 +63,28 @@ def main():
             s = S.StreamingEncoder(enc)
             data, width = x, a.chunk
         best = None
+        g = s.graph(data[..., :width]) if a.graph else None
+        if g is not None and data.shape[-1] % width:
+            raise SystemExit("--graph needs the stream length to be a multiple of the chunk")
         for _ in range(a.reps + 1):
-            s.reset()
+            s.reset() if g is None else g.reset()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             pushes = 0
             for i in range(0, data.shape[-1], width):
-                s.push(data[..., i:i + width])
+                if g is not None:
+                    g.push(data[..., i:i + width], check=False)
+                else:
+                    s.push(data[..., i:i + width])
                 pushes += 1
+            if g is not None:
+                g.check()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
     what = "decode" if a.decode else "encode"
-    print(f"stream {what} ({'prev' if a.prev else 'current'}): B {a.B} x {n / 24000:.1f} s, chunk {a.chunk} samples, "
+    mode = "prev" if a.prev else ("graph" if a.graph else "current")
+    print(f"stream {what} ({mode}): B {a.B} x {n / 24000:.1f} s, chunk {a.chunk} samples, "
           f"{pushes} pushes: {a.B * n / 24000 / best:.1f} audio-s/s, {1e3 * best / pushes:.2f} ms per push")
 
 
