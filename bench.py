@@ -183,8 +183,11 @@ def pmc_traffic(kernel: str):
 
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))  # r01_ < r01a_ < ... < r01h_
     for f in reversed(files):
-        d = json.load(open(f))["kernels"].get(kernel)
-        if d:
+        try:
+            d = json.load(open(f)).get("kernels", {}).get(kernel)
+        except (OSError, ValueError, AttributeError):  # a malformed summary must not take the bench down
+            continue
+        if d and "traffic_bytes_corrected" in d:
             return d["traffic_bytes_corrected"], d.get("mfma_util"), os.path.basename(f)
     return None, None, None
 

@@ -18,3 +18,22 @@ def test_kernel_peak_by_operand_planes():
     for name, peak in cases.items():
         got = bench.kernel_peak(name)[0]
         assert abs(got - peak) < 1e-9, (name, got, peak)
+
+
+def test_committed_pmc_summaries_are_readable():
+    """bench.py reads the newest profiles/*pmc_traffic.json for the roofline's `traffic`: every committed summary has
+    the tools/pmc_summary.py layout ({"kernels": {name: {"traffic_bytes_corrected", ...}}}), and the dominant h3
+    kernel resolves to a positive per-launch byte count."""
+    import glob
+    import json
+    import os
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(bench.__file__), "profiles", "*pmc_traffic.json")))
+    assert files
+    for f in files:
+        d = json.load(open(f))
+        assert isinstance(d.get("kernels"), dict), f
+        for name, v in d["kernels"].items():
+            assert "traffic_bytes_corrected" in v, (f, name)
+    traffic, util, src = bench.pmc_traffic("conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, true>")
+    assert traffic and traffic > 0 and src == os.path.basename(files[-1])
