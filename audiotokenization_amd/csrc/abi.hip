@@ -135,7 +135,12 @@ int bc_convT1d_fwd_ws(const float* x, const float* const* w_phases, const float*
                       const float* out_snake_alpha_exp, const float* out_snake_inv_beta, float* y,
                       float* y2, int B, int Cin, int Tin, int Cout, int Tout, int K, int stride,
                       int padding, int cfg, float* workspace, void* stream) {
-  if (!workspace)
+  // BC_CONVT_DIRECT_MAXS=s: strides <= s take the strided-store path even with a workspace (A/B timing)
+  static const int direct_maxs = [] {
+    const char* e = getenv("BC_CONVT_DIRECT_MAXS");
+    return e ? atoi(e) : 0;
+  }();
+  if (!workspace || stride <= direct_maxs)
     return bc_convT1d_fwd(x, w_phases, bias, out_snake_alpha_exp, out_snake_inv_beta, y, y2, B, Cin, Tin, Cout, Tout, K,
                           stride, padding, cfg, stream);
   if (!x || !w_phases || !y || B < 0 || Cin <= 0 || Tin < 0 || Cout <= 0 || Tout < 0 || K <= 0 || stride <= 0 ||
