@@ -333,8 +333,8 @@ def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
 
 @pytest.mark.parametrize("lprec", ["h3", "x6"])
 def test_reslstm_half_split_bit_identical(dev, lprec):
-    """The persistent recurrence runs a launch of <= 32 clips as two halves of 16 (NTH = 1) and a launch of 33-64
-    clips as two halves of 32: a clip's gates are summed over the same K ranges, waves and MFMA chains either way,
+    """The persistent recurrence runs a launch of <= 32 clips as two halves of 16 (NTH = 1; half 1 empty at <= 16 clips)
+    and a launch of 33-64 clips as two halves of 32: a clip's gates are summed over the same K ranges, waves and MFMA chains either way,
     so in x6 (exact per-element operand splits everywhere) the first 32 / 20 clips of a 64-clip batch come out
     bit-identical when run alone.  In h3 the input projection's block scales span the clips of a column tile, so
     there only agreement at the 22-bit operand level is asserted; both match the oracle."""
@@ -354,15 +354,21 @@ def test_reslstm_half_split_bit_identical(dev, lprec):
         full = m(xd).cpu()
         y32 = m(xd[:32].contiguous()).cpu()
         y20 = m(xd[:20].contiguous()).cpu()
+        # <= 16 clips: half 1 is empty (its chain still runs and hides half 0's hand-off latency)
+        small = {n: m(xd[:n].contiguous()).cpu() for n in (16, 5, 1)}
         assert L.load().bc_lstm_status(1) == 0
     finally:
         L._mode = old
     if lprec == "x6":
         assert torch.equal(y32, full[:32]), (y32 - full[:32]).abs().max()
         assert torch.equal(y20, full[:20]), (y20 - full[:20]).abs().max()
+        for n, y in small.items():
+            assert torch.equal(y, full[:n]), (n, (y - full[:n]).abs().max())
     else:
         assert_close_rel(y32, full[:32], 2e-6, "h3 lstm 32 vs 64 clips")
         assert_close_rel(y20, full[:20], 2e-6, "h3 lstm 20 vs 64 clips")
+        for n, y in small.items():
+            assert_close_rel(y, full[:n], 2e-6, f"h3 lstm {n} vs 64 clips")
     want = O.res_lstm(x[:20], sd, "", 2)
     assert_close_rel(y20, want, 2e-5, f"lstm {lprec} 20 clips")
 
