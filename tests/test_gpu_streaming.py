@@ -180,3 +180,27 @@ def test_stream_graph_equals_eager_stream(dev, sprec):
         g.check()
     finally:
         L._mode = old
+
+
+def test_stream_bf16_equals_whole_pass(dev):
+    """bf16 conv products (config 5's arithmetic) in the stream: one bf16 plane per operand, no block scales, so the
+    products do not depend on the tiling and the encode / decode streams equal the bf16 whole-sequence pass bit for
+    bit, like x6 (the fidelity of bf16 itself is test_gpu_configs.py's concern)."""
+    from audiotokenization_amd.streaming import StreamingDecoder
+
+    old = L.precision_mode()
+    try:
+        L.set_precision("bf16")
+        enc, dec, *_ = build_models("default", device=dev, causal=True)
+        x = torch.from_numpy(synth.synth_clips(2, 6000, clip0=41)).unsqueeze(1).to(dev)
+        with torch.no_grad():
+            full = enc(x)
+            a = StreamingEncoder(enc).encode(x, 1200)
+            post = dec(full, vq=True)[0]
+            wav = dec(post, vq=False)
+            w = StreamingDecoder(dec).decode(post, 7)
+            torch.cuda.synchronize()
+    finally:
+        L._mode = old
+    print(f"bf16 stream: encode {max_rel_err(a, full):.2e}, decode {max_rel_err(w, wav):.2e} vs the whole pass")
+    assert torch.equal(a, full) and torch.equal(w, wav)
