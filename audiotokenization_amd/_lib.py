@@ -28,6 +28,7 @@ L = C.c_longlong
 _SIGS = {
     "bc_abi_version": (I, []),
     "bc_conv1d_select_cfg": (I, [I, I, I, I, I, I]),
+    "bc_conv1d_select_cfg_n": (I, [I, I, I, I, I, I, I, I]),
     "bc_conv1d_packed_floats": (L, [I, I, I, I]),
     "bc_conv1d_pack": (I, [P, P, I, I, I, I]),
     "bc_conv1d_fwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
@@ -73,7 +74,7 @@ _SIGS = {
     "bc_debug_selftest": (I, [I, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 14  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 15  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 

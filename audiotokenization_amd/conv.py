@@ -110,8 +110,8 @@ class Conv1dWN(_WNParams, nn.Module):
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return torch.from_numpy(packed).to(device), bias
         if not hasattr(self, "_cache_as"):
-            self._cache_as = _DeviceCache()
-        return self._cache_as.get(_pkey(*self._params()) + (str(device), cfg), build)
+            self._cache_as = {}
+        return self._cache_as.setdefault(cfg, _DeviceCache()).get(_pkey(*self._params()) + (str(device), cfg), build)
 
     def pad_left(self) -> int:
         return self.causal_pad if self.causal_pad is not None else self.padding
@@ -141,6 +141,12 @@ class Conv1dWN(_WNParams, nn.Module):
             if tuple(residual.shape) != (B, self.out_channels, Tout):
                 raise ValueError(f"residual shape {tuple(residual.shape)} != output {(B, self.out_channels, Tout)}")
         sa, sb = _epilogue_args(out_snake, dual)
+        if Tout <= 128 and self.kernel_size > 1:  # a narrow launch may take a narrower tile
+            cfg_n = L.load().bc_conv1d_select_cfg_n(self.out_channels, Cin, self.kernel_size, self.stride,
+                                                    self.dilation, L.precision_mode(), B, Tout)
+            if cfg_n >= 0 and cfg_n != cfg:
+                wp, bias = self.packed_as(cfg_n, x.device)
+                cfg = cfg_n
         tm = L.active_timer()
         ev = tm.begin() if tm is not None else None
         out = ops.load().conv1d(x, wp, bias, residual, sa, sb, self.out_channels, Tout, self.kernel_size, self.stride,
@@ -205,16 +211,28 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
         self.causal_crop = 0  # set by CausalConvTranspose1d
         ref = nn.ConvTranspose1d(in_channels, out_channels, self.kernel_size, stride, bias=bias)
         _wn_init(self, ref.weight, ref.bias)
-        self._cache = _DeviceCache()
+        self._cache = {}  # cfg -> _DeviceCache (the shape table's tile and narrow-launch tiles)
 
-    def prepared(self, device):
+    def phase_cfg(self, B: int = 0, Tin: int = 0) -> int:
+        """Tile of the per-phase convs (Kp taps, stride 1); with the launch's B and input length, the narrow-launch
+        choice (bc_conv1d_select_cfg_n: each phase writes about Tin columns per clip)."""
+        lib = L.load()
+        Kp = lib.bc_convT1d_phase_taps(self.kernel_size, self.stride)
+        cfg = L.conv_cfg(self.out_channels, self.in_channels, Kp, 1, 1, L.precision_mode())
+        if B > 0 and 0 < Tin <= 128:
+            n = lib.bc_conv1d_select_cfg_n(self.out_channels, self.in_channels, Kp, 1, 1, L.precision_mode(), B, Tin)
+            cfg = n if n >= 0 else cfg
+        return cfg
+
+    def prepared(self, device, cfg: Optional[int] = None):
+        cfg = self.phase_cfg() if cfg is None else cfg
+
         def build():
             w = self.folded_weight()  # (Cin, Cout, K)
             Cin, Cout, K = w.shape
             s = self.stride
             lib = L.load()
             Kp = lib.bc_convT1d_phase_taps(K, s)
-            cfg = L.conv_cfg(Cout, Cin, Kp, 1, 1, L.precision_mode())
             n = L.checked_size(lib.bc_conv1d_packed_floats(Cout, Cin, Kp, cfg),
                                f"bc_conv1d_packed_floats({Cout}, {Cin}, {Kp}, cfg {cfg})")
             wt = w.permute(1, 0, 2).contiguous()  # (Cout, Cin, K)
@@ -230,7 +248,7 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
                 phases.append(torch.from_numpy(packed).to(device))
             bias = _cpu(self.bias).contiguous().to(device) if self.bias is not None else None
             return phases, L.ptr_array([p.data_ptr() for p in phases]), bias, cfg
-        return self._cache.get(_pkey(*self._params()) + (str(device), L.precision_mode()), build)
+        return self._cache.setdefault(cfg, _DeviceCache()).get(_pkey(*self._params()) + (str(device), cfg), build)
 
     def out_len(self, T: int) -> int:
         full = (T - 1) * self.stride - 2 * self.padding + self.kernel_size + self.output_padding
@@ -241,7 +259,7 @@ class ConvTranspose1dWN(_WNParams, nn.Module):
         B, Cin, T = x.shape
         if Cin != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
-        phases, _, bias, cfg = self.prepared(x.device)
+        phases, _, bias, cfg = self.prepared(x.device, self.phase_cfg(B, T))
         Tout = self.out_len(T)
         if Tout <= 0:
             raise ValueError(f"input length {T} too short for this transposed convolution")

@@ -17,6 +17,18 @@ int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int
   return conv_select_cfg(Cout, Cin, K, stride, dilation, mode);
 }
 
+int bc_conv1d_select_cfg_n(int Cout, int Cin, int K, int stride, int dilation, int mode, int B, int Tout) {
+  const int cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode);
+  if (cfg < 0 || mode < 1) return cfg;
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return x6_narrow_cfg(cfg, Cout, K, stride, dilation, mode == 1 ? 3 : mode == 2 ? 1 : 2, B, Tout, cus);
+}
+
 // a cfg is acceptable for a shape if some precision mode selects it
 // Any valid tile id may run a conv (the select functions give the tuned choice; tools/conv_bench.py
 // times others): the kernel launchers reject a tile the shape does not fit (BC_ERR_UNSUPPORTED).

@@ -36,6 +36,7 @@ struct ConvArgs {
 int conv_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode = 0);
 bool conv_cfg_valid(int cfg_id);
 int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes);
+int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int Tout, int cus);
 bool x6_cfg_valid(int cfg);
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg);
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg);

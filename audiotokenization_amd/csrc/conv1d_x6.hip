@@ -227,6 +227,35 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
   return x6_select_tile(Cout, Cin, K, s, d, planes);
 }
 
+// Narrow launches (a stream's chunk, a small batch): the shape tables above assume thousands of output columns per
+// clip.  The 16-wave 192 x 256 tile computes 256 columns per clip whatever Tout is, so a stride-1 multi-tap conv (or a
+// phase-decomposed strided one, whose phase conv has K / s taps) with Tout <= 128 moves to a tile whose width covers
+// Tout (64 or 128 columns), and to fewer rows (96 / 32) when 192-row
+// tiles would leave the CUs idle.  Measured on five stream / small-batch shapes, 1.3-2.5x per launch, the rule's pick
+// the fastest tile on each (profiles/r04s_narrow_sweep.txt).  Same K order per output: x6 and bf16 results do not
+// depend on the tile; h3's block scales follow the staged tile (fp32 rounding level).  BC_X6_NARROW=0 disables it.
+int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int Tout, int cus) {
+  static const bool on = [] {
+    const char* e = getenv("BC_X6_NARROW");
+    return !(e && atoi(e) == 0);
+  }();
+  const int base = planes == 3 ? 0 : planes == 1 ? 100 : 200;
+  if (cfg >= 1000) {  // a phase-decomposed strided conv: the stride-1 conv over ps phase rows per channel
+    const int ps = cfg / 1000;
+    if (s != ps || d != 1) return cfg;
+    const int inner = x6_narrow_cfg(cfg % 1000, Cout, (K + s - 1) / s, 1, 1, planes, B, Tout, cus);
+    return 1000 * ps + inner;
+  }
+  if (!on || s != 1 || K < 2 || Tout > 128 || Tout <= 0 || B <= 0 || cfg - base != 122) return cfg;
+  auto nwg = [&](int bm) { return (long long)((Cout + bm - 1) / bm) * B; };
+  const bool fill192 = Cout % 192 == 0 && nwg(192) >= cus;
+  int tile;
+  if (Tout <= 64) tile = fill192 ? 15 : (Cout % 96 == 0 ? 16 : 12);
+  else tile = fill192 ? 14 : 12;
+  if (x6_ncol(kX6Tiles[tile], K, 1, d) > 32 * X6_MAXCOL_ITERS) return cfg;
+  return base + 100 + tile;
+}
+
 static int x6_select_tile(int Cout, int Cin, int K, int s, int d, int planes) {
   int order[8];
   bool occ4[8] = {false};

@@ -162,7 +162,7 @@ class StreamingDecoder(StreamingEncoder):
             raise NotImplementedError(f"streaming transposed conv needs kernel_size % stride == 0 (k={K}, s={s})")
         c = K // s - 1  # input frames of history an output block needs
         x = self._window(id(conv), h, c, act)
-        phases, _, bias, cfg = conv.prepared(x.device)
+        phases, _, bias, cfg = conv.prepared(x.device, conv.phase_cfg(x.shape[0], x.shape[-1]))
         # full length (n + c - 1) s + K; padding c * s crops c * s on both sides: the n * s outputs of this chunk
         out = ops.load().conv_transpose1d(x, phases, bias, None, None, conv.out_channels, h.shape[-1] * s, K, s, c * s,
                                           cfg, False)

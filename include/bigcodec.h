@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 14
+#define BC_ABI_VERSION 15
 
 int bc_abi_version(void);
 
@@ -55,6 +55,11 @@ int bc_abi_version(void);
  * out_snake_alpha_exp[c] = exp(alpha[c]); out_snake_inv_beta[c] = 1/(exp(beta[c]) + 1e-9).
  * Limits: Cin*Tin*4 < 2^31 bytes per clip. */
 int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int mode);
+/* bc_conv1d_select_cfg_n: the same choice for a launch of B clips with Tout output columns each: a stride-1
+ *   multi-tap conv with Tout <= 128 (a streaming chunk, a small batch) may take a narrower tile than the shape
+ *   table's (ABI 15; x6 / bf16 results are the same on either tile, h3 agrees to fp32 rounding).  The packed
+ *   weights must be packed for the returned cfg. */
+int bc_conv1d_select_cfg_n(int Cout, int Cin, int K, int stride, int dilation, int mode, int B, int Tout);
 long long bc_conv1d_packed_floats(int Cout, int Cin, int K, int cfg);
 int bc_conv1d_pack(const float* w_host, float* packed_host, int Cout, int Cin, int K, int cfg);
 int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, const float* residual,

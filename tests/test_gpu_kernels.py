@@ -861,3 +861,49 @@ def test_b4_staging_bit_identical_to_single_float(dev, Cin, Cout, K, d, T, cfg):
         assert_close_rel(outs[0], want, tol, f"{prec} cfg {cfg}")
     finally:
         L._mode = old
+
+
+@pytest.mark.parametrize("Cin,Cout,d,B,T", [(768, 768, 1, 16, 25), (384, 384, 3, 4, 125), (1024, 1536, 1, 3, 5),
+                                           (192, 192, 9, 2, 60), (1536, 1536, 1, 64, 24), (768, 768, 9, 64, 120)])
+@pytest.mark.parametrize("prec", ["x6", "bf16", "h3"])
+def test_narrow_launch_tile(dev, Cin, Cout, d, B, T, prec):
+    """bc_conv1d_select_cfg_n (ABI 15): a stride-1 k7 conv with <= 128 output columns per clip (a streaming chunk, a
+    small batch) leaves the 16-wave 192 x 256 tile for a narrower one; the module picks it by itself.  The same K
+    order per output makes x6 and bf16 results bit-identical on either tile; h3 (block scales per staged tile) agrees
+    to fp32 rounding and matches the fp64 oracle at the conv tolerance."""
+    old = L.precision_mode()
+    L.set_precision(prec)
+    try:
+        g = torch.Generator().manual_seed(Cin + 7 * d + T)
+        K, pad = 7, 3 * d
+        m = CV.WNConv1d(Cin, Cout, kernel_size=K, dilation=d, padding=pad)
+        conv = _rand_wn_conv(m, g)
+        x = torch.randn(B, Cin, T, generator=g)
+        sd = {k: v.detach() for k, v in conv.state_dict().items()}
+        m.to(dev)
+        xd = x.to(dev)
+        lib = L.load()
+        wide = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, d, L.precision_mode())
+        narrow = lib.bc_conv1d_select_cfg_n(Cout, Cin, K, 1, d, L.precision_mode(), B, T)
+        assert wide % 100 == 22 and narrow != wide, (wide, narrow)
+        st = torch.cuda.current_stream().cuda_stream
+        outs = {}
+        for cfg in (wide, narrow):
+            wp, bias = m.packed_as(cfg, dev)
+            y = torch.empty(B, Cout, T, device=dev)
+            L.call("bc_conv1d_fwd", xd.data_ptr(), wp.data_ptr(), L.ptr(bias), 0, 0, 0, y.data_ptr(), 0,
+                   B, Cin, T, Cout, T, K, 1, d, pad, 0, cfg, st)
+            outs[cfg] = y
+        via_module = m(xd)
+        torch.cuda.synchronize()
+    finally:
+        L._mode = old
+    a, b = outs[wide].cpu(), outs[narrow].cpu()
+    assert torch.equal(via_module.cpu(), b), "the module runs the narrow tile"
+    if prec in ("x6", "bf16"):
+        assert torch.equal(a, b), (a - b).abs().max()
+    else:
+        assert_close_rel(b, a, 2e-6, "h3 narrow vs 16-wave tile")
+    if prec == "h3":
+        want = O.conv(x, sd, "", K, 1, pad, d, False)
+        assert_close_rel(b, want, 3e-6 * max(1.0, np.sqrt(Cin * K / 64)), "h3 narrow tile vs oracle")
