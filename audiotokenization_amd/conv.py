@@ -141,7 +141,7 @@ class Conv1dWN(_WNParams, nn.Module):
             if tuple(residual.shape) != (B, self.out_channels, Tout):
                 raise ValueError(f"residual shape {tuple(residual.shape)} != output {(B, self.out_channels, Tout)}")
         sa, sb = _epilogue_args(out_snake, dual)
-        if Tout <= 128 and self.kernel_size > 1:  # a narrow launch may take a narrower tile
+        if Tout <= 128:  # a narrow launch may take a narrower tile
             cfg_n = L.load().bc_conv1d_select_cfg_n(self.out_channels, Cin, self.kernel_size, self.stride,
                                                     self.dilation, L.precision_mode(), B, Tout)
             if cfg_n >= 0 and cfg_n != cfg:

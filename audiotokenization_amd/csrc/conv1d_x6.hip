@@ -230,9 +230,10 @@ int x6_select_cfg(int Cout, int Cin, int K, int s, int d, int planes) {
 // Narrow launches (a stream's chunk, a small batch): the shape tables above assume thousands of output columns per
 // clip.  The 16-wave 192 x 256 tile computes 256 columns per clip whatever Tout is, so a stride-1 multi-tap conv (or a
 // phase-decomposed strided one, whose phase conv has K / s taps) with Tout <= 128 moves to a tile whose width covers
-// Tout (64 or 128 columns), and to fewer rows (96 / 32) when 192-row
-// tiles would leave the CUs idle.  Measured on five stream / small-batch shapes, 1.3-2.5x per launch, the rule's pick
-// the fastest tile on each (profiles/r04s_narrow_sweep.txt).  Same K order per output: x6 and bf16 results do not
+// Tout (64 or 128 columns), and to fewer rows (96 / 32) when 192-row tiles would leave the CUs idle; a pointwise conv
+// takes a 64-column tile up to 128 columns.  Measured on five k7 and four pointwise stream / small-batch shapes: the
+// rule picks the fastest tile on each, 1.3-2.5x per k7 launch, 1.1-2.2x per pointwise one
+// (profiles/r04s_narrow_sweep.txt, r04u_pw_narrow_sweep.txt).  Same K order per output: x6 and bf16 results do not
 // depend on the tile; h3's block scales follow the staged tile (fp32 rounding level).  BC_X6_NARROW=0 disables it.
 int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int Tout, int cus) {
   static const bool on = [] {
@@ -246,7 +247,14 @@ int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int
     const int inner = x6_narrow_cfg(cfg % 1000, Cout, (K + s - 1) / s, 1, 1, planes, B, Tout, cus);
     return 1000 * ps + inner;
   }
-  if (!on || s != 1 || K < 2 || Tout > 128 || Tout <= 0 || B <= 0 || cfg - base != 122) return cfg;
+  if (!on || s != 1 || Tout > 128 || Tout <= 0 || B <= 0) return cfg;
+  if (K == 1) {  // pointwise: 64-column tiles win up to 128 columns (two n-tiles per clip), 192 rows when they fill
+    if (cfg - base != 114 && cfg - base != 122) return cfg;
+    const long long n192 = (long long)((Cout + 191) / 192) * ((Tout + 63) / 64) * B;
+    const int tile = (Cout % 192 == 0 && n192 >= cus) ? 15 : (Cout % 96 == 0 ? 16 : -1);
+    return tile < 0 ? cfg : base + 100 + tile;
+  }
+  if (cfg - base != 122) return cfg;
   auto nwg = [&](int bm) { return (long long)((Cout + bm - 1) / bm) * B; };
   const bool fill192 = Cout % 192 == 0 && nwg(192) >= cus;
   int tile;
