@@ -356,7 +356,9 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
   const int cfg = conv_select_cfg(4 * H, Cin, 1, 1, 1, mode);
   int rc;
-  if (psplit && g_lstm_presplit && cfg == 322 && pw_presplit_ok(4 * H, Cin, tb))
+  // (few columns, e.g. a streaming chunk: presplit_b walks every chunk of a 256-column tile in one workgroup, a fixed
+  // ~220 us, so below 32 tiles the plain 322 launch, bit-identical, is faster; profiles/r04v_presplit_narrow.txt)
+  if (psplit && g_lstm_presplit && cfg == 322 && (tb >= 32 * 256 || g_lstm_presplit == 2) && pw_presplit_ok(4 * H, Cin, tb))
     rc = pw_presplit_launch(a, psplit, st);  // same planes, scales and MFMA chains as cfg 322: bit-identical
   else
     rc = conv_launch(a, 1, cfg, st);
@@ -574,10 +576,11 @@ int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream) 
 }  // extern "C"
 
 // Diagnostics only (not part of include/bigcodec.h): run the unidirectional ResLSTM's input projection on the
-// pre-split GEMM (1, the default) or on conv1d_x6_kernel (0); returns the previous setting.
+// pre-split GEMM from 32 column tiles up (1, the default), at every size (2: the bit-identity test's small shapes)
+// or on conv1d_x6_kernel (0); returns the previous setting.
 extern "C" int bc_debug_set_lstm_presplit(int on) {
   const int old = g_lstm_presplit;
-  g_lstm_presplit = on ? 1 : 0;
+  g_lstm_presplit = on == 2 ? 2 : on ? 1 : 0;
   return old;
 }
 

@@ -318,7 +318,7 @@ def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
         sd = {k: v.detach() for k, v in m.state_dict().items()}
         m.to(dev)
         xd = x.to(dev)
-        prev = lib.bc_debug_set_lstm_presplit(1)
+        prev = lib.bc_debug_set_lstm_presplit(2)  # the pre-split GEMM at any size (below 32 column tiles too)
         y_ps = m(xd).cpu()
         lib.bc_debug_set_lstm_presplit(0)
         y_x6 = m(xd).cpu()
