@@ -254,12 +254,17 @@ int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int
     const int tile = (Cout % 192 == 0 && n192 >= cus) ? 15 : (Cout % 96 == 0 ? 16 : -1);
     return tile < 0 ? cfg : base + 100 + tile;
   }
-  if (cfg - base != 122) return cfg;
-  auto nwg = [&](int bm) { return (long long)((Cout + bm - 1) / bm) * B; };
-  const bool fill192 = Cout % 192 == 0 && nwg(192) >= cus;
   int tile;
-  if (Tout <= 64) tile = fill192 ? 15 : (Cout % 96 == 0 ? 16 : 12);
-  else tile = fill192 ? 14 : 12;
+  if (cfg - base == 121) {  // the 256 x 256 tile (Cout % 256 == 0, e.g. the encoder's final k3): 128 x 64 up to 64
+    if (Tout > 64 || Cout % 128 != 0) return cfg;  // columns (k3 1536 -> 1024: 0.377 -> 0.176 ms at 16 x 6 columns,
+    tile = 17;                                      // 0.411 -> 0.245 at 64 x 24; profiles/r04y_k3_sweep.txt)
+  } else {
+    if (cfg - base != 122) return cfg;
+    auto nwg = [&](int bm) { return (long long)((Cout + bm - 1) / bm) * B; };
+    const bool fill192 = Cout % 192 == 0 && nwg(192) >= cus;
+    if (Tout <= 64) tile = fill192 ? 15 : (Cout % 96 == 0 ? 16 : 12);
+    else tile = fill192 ? 14 : 12;
+  }
   if (x6_ncol(kX6Tiles[tile], K, 1, d) > 32 * X6_MAXCOL_ITERS) return cfg;
   return base + 100 + tile;
 }

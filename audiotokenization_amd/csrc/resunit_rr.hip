@@ -799,13 +799,18 @@ static bool strip_enabled() {
   }();
   return v;
 }
-static int strip_nblk() {
+// Blocks per strip: 8 (weights and halo reused along a strip), fewer when B * blocks / 8 would leave CUs without a
+// strip (a streaming chunk, a small batch: 16 clips x 10 blocks are 32 strips of 8 for 256 CUs); the per-block
+// arithmetic does not depend on the partition.  BC_RU_STRIP_NBLK fixes it.
+static int strip_nblk(long long B, int nbt, int cus) {
   static const int v = [] {
     const char* s = getenv("BC_RU_STRIP_NBLK");
     const int n = s ? atoi(s) : 0;
-    return n > 0 ? n : 8;
+    return n > 0 ? n : 0;
   }();
-  return v;
+  if (v > 0) return v;
+  const long long fill = cus > 0 ? B * nbt / cus : 8;
+  return (int)std::max<long long>(1, std::min<long long>(8, fill));
 }
 static bool strip_ok(int C, int d) { return strip_enabled() && C == RS_C && (d == 1 || d == 3 || d == 9); }
 
@@ -822,7 +827,7 @@ static int strip_cus() {
 template <int D>
 static int launch_strip(RSArgs& r, ConvArgs& e, int B, hipStream_t st) {
   const int nbt = (r.T + RS_BN - 1) / RS_BN;
-  r.nblk = strip_nblk();
+  r.nblk = strip_nblk(B, nbt, strip_cus());
   r.nstrip = (nbt + r.nblk - 1) / r.nblk;
   const long long nwork = (long long)B * r.nstrip;
   if (nwork <= 0) return BC_OK;
