@@ -17,16 +17,20 @@ int bc_conv1d_select_cfg(int Cout, int Cin, int K, int stride, int dilation, int
   return conv_select_cfg(Cout, Cin, K, stride, dilation, mode);
 }
 
-int bc_conv1d_select_cfg_n(int Cout, int Cin, int K, int stride, int dilation, int mode, int B, int Tout) {
-  const int cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode);
-  if (cfg < 0 || mode < 1) return cfg;
+static int device_cus() {
   static const int cus = [] {
     int dev = 0, v = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 256;
     return v > 0 ? v : 256;
   }();
-  return x6_narrow_cfg(cfg, Cout, K, stride, dilation, mode == 1 ? 3 : mode == 2 ? 1 : 2, B, Tout, cus);
+  return cus;
+}
+
+int bc_conv1d_select_cfg_n(int Cout, int Cin, int K, int stride, int dilation, int mode, int B, int Tout) {
+  const int cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode);
+  if (cfg < 0 || mode < 1) return cfg;
+  return x6_narrow_cfg(cfg, Cout, K, stride, dilation, mode == 1 ? 3 : mode == 2 ? 1 : 2, B, Tout, device_cus());
 }
 
 // a cfg is acceptable for a shape if some precision mode selects it
@@ -354,6 +358,7 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   a.Cin = Cin; a.Tin = (int)tb; a.Cout = 4 * H; a.Nout = (int)tb;
   a.K = 1; a.s = 1; a.d = 1; a.pl = 0;
   a.yT = (int)tb; a.ostride = 1; a.ooff = 0; a.epi = 0;
+  // W_ih is packed for the shape table's cfg (include/bigcodec.h), so the narrow-launch tiles do not apply here
   const int cfg = conv_select_cfg(4 * H, Cin, 1, 1, 1, mode);
   int rc;
   // (few columns, e.g. a streaming chunk: presplit_b walks every chunk of a 256-column tile in one workgroup, a fixed
