@@ -75,6 +75,7 @@ __device__ __forceinline__ int vq_search(const float (&e)[VQ_DIM], float se,
     for (int q = threadIdx.x; q < cn * VQ_DIM; q += blockDim.x) lds_cb[q] = cbn[(long long)c0 * VQ_DIM + q];
     for (int q = threadIdx.x; q < cn; q += blockDim.x) lds_sq[q] = csq[c0 + q];
     __syncthreads();
+#pragma unroll 4
     for (int k = 0; k < cn; ++k) {
       const float* c = lds_cb + k * VQ_DIM;
       float dot = 0.f;
@@ -110,11 +111,23 @@ __global__ void __launch_bounds__(256) vq_fwd_kernel(
   const int b = (int)(nn / T), t = (int)(nn % T);
   const float* zb = z + (long long)b * D * T + t;
 
-  // in_proj: z_e[j] = sum_d W[j][d] z[d] + bias[j]
+  // in_proj: z_e[j] = sum_d W[j][d] z[d] + bias[j]; the z column is loaded 16 channels at a time, so 16 loads are in
+  // flight instead of one (one wave per SIMD here: each load's latency was exposed); the FMA chains keep d's order
   float ze[VQ_DIM];
 #pragma unroll
   for (int q = 0; q < VQ_DIM; ++q) ze[q] = 0.f;
-  for (int d = 0; d < D; ++d) {
+  constexpr int ZU = 16;
+  int d = 0;
+  for (; d + ZU <= D; d += ZU) {
+    float zv[ZU];
+#pragma unroll
+    for (int j = 0; j < ZU; ++j) zv[j] = zb[(long long)(d + j) * T];
+#pragma unroll
+    for (int j = 0; j < ZU; ++j)
+#pragma unroll
+      for (int q = 0; q < VQ_DIM; ++q) ze[q] = fmaf(w_in[q * D + d + j], zv[j], ze[q]);
+  }
+  for (; d < D; ++d) {
     const float zv = zb[(long long)d * T];
 #pragma unroll
     for (int q = 0; q < VQ_DIM; ++q) ze[q] = fmaf(w_in[q * D + d], zv, ze[q]);
