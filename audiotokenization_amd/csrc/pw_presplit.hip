@@ -43,9 +43,9 @@ __global__ void __launch_bounds__(256) presplit_b_kernel(const float* __restrict
   const int n = j * PS_BN + 4 * lane;
   __shared__ unsigned wmax[4];
   float xs = 1.f;
-  for (int c = 0; c < nch; ++c) {
-    float v[8][4];
-    unsigned m = 0;
+  // chunk c + 1's rows are loaded while chunk c is reduced and split (two register sets): the per-chunk work is the
+  // same, the loads of the next chunk no longer wait behind this chunk's two barriers
+  auto load = [&](int c, float (&v)[8][4]) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int ch = c * X6_BKC + 8 * w + k;
@@ -58,12 +58,17 @@ __global__ void __launch_bounds__(256) presplit_b_kernel(const float* __restrict
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[k][r] = (ch < Cin && n + r < N) ? row[n + r] : 0.f;
       }
+    }
+  };
+  auto body = [&](int c, const float (&v)[8][4]) {
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const unsigned u = __float_as_uint(fabsf(v[k][r]));
         m = m > u ? m : u;
       }
-    }
     m = wave_max_u32(m);
     if (lane == 0) wmax[w] = m;
     __syncthreads();
@@ -84,6 +89,16 @@ __global__ void __launch_bounds__(256) presplit_b_kernel(const float* __restrict
       const int off = col * 64 + 16 * (w ^ ((col >> 1) & 3));
       *reinterpret_cast<u32x4_t*>(pb + off) = (u32x4_t){h[0], h[1], h[2], h[3]};
       *reinterpret_cast<u32x4_t*>(pb + PS_PLANE + off) = (u32x4_t){l[0], l[1], l[2], l[3]};
+    }
+  };
+  float va[8][4], vb[8][4];
+  if (nch > 0) load(0, va);
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) load(c + 1, vb);
+    body(c, va);
+    if (c + 1 < nch) {
+      if (c + 2 < nch) load(c + 2, va);
+      body(c + 1, vb);
     }
   }
 }
