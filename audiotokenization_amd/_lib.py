@@ -27,6 +27,7 @@ L = C.c_longlong
 # name -> (restype, argtypes)
 _SIGS = {
     "bc_abi_version": (I, []),
+    "bc_build_digest": (C.c_char_p, []),
     "bc_conv1d_select_cfg": (I, [I, I, I, I, I, I]),
     "bc_conv1d_select_cfg_n": (I, [I, I, I, I, I, I, I, I]),
     "bc_conv1d_packed_floats": (L, [I, I, I, I]),
@@ -74,7 +75,7 @@ _SIGS = {
     "bc_debug_selftest": (I, [I, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 15  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 16  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -356,18 +357,18 @@ def resunit_kernel_name(cfg: int, C: int = 0, dilation: int = 1) -> str:
     return _kernel_name("bc_resunit_kernel_name", cfg, C, dilation)
 
 
-# Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = fp32-accurate 3xbf16 split MFMA ("x6":
-# same accuracy class as fp32 — see DESIGN.md §4 — at 2.65x the MFMA ceiling),
+# Precision mode of the conv GEMMs: 0 = native fp32 MFMA, 1 = "x6", the default: both fp32 operands split EXACTLY
+# into three bf16 terms (24-bit operands, the reference's fp32 width; vq/module.py:45-48, 65), six bf16 products per
+# pair accumulated in fp32, at 2.65x the native fp32 MFMA ceiling,
 # 2 = plain bf16 products (BASELINE config 5; NOT index-exact; the ResLSTM runs on h3: fp32-class, 22-bit operands),
-# 3 = "h3", the default: two fp16 planes per operand with power-of-two block scaling, three products
-# (fp32-class accuracy, measured below the fp32 MFMA kernel's error) at half the x6
-# MFMA count.
+# 3 = "h3": two fp16 planes per operand with power-of-two block scaling (22-bit operands: NARROWER than the
+# reference's fp32), three products, at half the x6 MFMA count (opt-in: BIGCODEC_PRECISION=h3).
 PRECISIONS = {"fp32": 0, "x6": 1, "bf16": 2, "h3": 3}
-_mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "h3")]
+_mode = PRECISIONS[os.environ.get("BIGCODEC_PRECISION", "x6")]
 
 
 def set_precision(name: str) -> None:
-    """Select the conv GEMM arithmetic ('fp32' or 'x6'); prepared weights re-pack on next use."""
+    """Select the conv GEMM arithmetic ('x6' default, 'fp32', 'h3', 'bf16'); prepared weights re-pack on next use."""
     global _mode
     if name not in PRECISIONS:
         raise ValueError(f"unknown precision {name!r}: expected one of {sorted(PRECISIONS)}")

@@ -51,9 +51,22 @@ def _paths(debug: bool):
     return BUILD, LIB, CFLAGS
 
 
-def stamp_path(debug: bool = False) -> str:
-    """The built library's source digest (the debug one next to its library: _debug/_build stays off the GPU box)."""
-    return os.path.join(DEBUG_DIR, "stamp") if debug else os.path.join(BUILD, "stamp")
+DIGEST_MARK = b"BC_BUILD_DIGEST="
+
+
+def lib_digest(lib_path: str) -> str | None:
+    """The source digest compiled INTO a built library (bc_build_digest; the marker string in its .rodata), read
+    from the file without loading it; None for a missing file or a library without the marker."""
+    try:
+        with open(lib_path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(DIGEST_MARK)
+    if i < 0:
+        return None
+    d = data[i + len(DIGEST_MARK):i + len(DIGEST_MARK) + 64]
+    return d.decode() if len(d) == 64 and all(c in b"0123456789abcdef" for c in d) else None
 
 
 def _digest(flags=None) -> str:
@@ -71,12 +84,11 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False) -> st
     """Compile (if sources changed) and return the path of libbigcodec_hip.so (debug: the bounds-checked build)."""
     build_dir, lib_path, flags = _paths(debug)
     os.makedirs(build_dir, exist_ok=True)
-    stamp = stamp_path(debug)
     dig = _digest(flags)
-    if not force and os.path.exists(lib_path) and os.path.exists(stamp):
-        with open(stamp) as fh:
-            if fh.read().strip() == dig:
-                return lib_path
+    # the digest lives in the library itself (no side stamp file that a checkout could leave agreeing with the
+    # sources while the git-ignored .so is another tree's: ADVICE r04)
+    if not force and lib_digest(lib_path) == dig:
+        return lib_path
     hipcc = _hipcc()
 
     common = hashlib.sha256()  # every header (any source may include any of them) + the flags
@@ -109,14 +121,22 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False) -> st
 
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8, 16)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
+    # bc_build_digest (include/bigcodec.h): the digest of exactly these sources and flags, compiled in
+    dsrc, dobj = os.path.join(build_dir, "digest.c"), os.path.join(build_dir, "digest.o")
+    with open(dsrc, "w") as fh:
+        fh.write(f'static const char bc_digest_str[] = "{DIGEST_MARK.decode()}{dig}";\n'
+                 f'const char* bc_build_digest(void) {{ return bc_digest_str + {len(DIGEST_MARK)}; }}\n')
+    res = subprocess.run([os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-c", dsrc, "-o", dobj], capture_output=True,
+                         text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"digest object failed:\n{res.stderr}")
+    objs.append(dobj)
     tmp = lib_path + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-soname,libbigcodec_hip.so", *objs, "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stderr}")
     os.replace(tmp, lib_path)
-    with open(stamp, "w") as fh:
-        fh.write(dig)
     return lib_path
 
 

@@ -22,9 +22,13 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 15
+#define BC_ABI_VERSION 16
 
 int bc_abi_version(void);
+/* bc_build_digest: sha256 (64 hex characters) of the sources, headers and compiler flags this library was built
+ * from (ABI 16).  build_lib.py compiles it in and rebuilds when it differs from the tree's; bench.py reports a
+ * committed PMC profile's traffic only when the profile was taken on a library with the running one's digest. */
+const char* bc_build_digest(void);
 
 /* ---- Conv1d (weight-normed, fused residual / tanh / next-Snake epilogue) --------------------------
  * Replaces: F.pad + conv1d of CausalConv1d.forward (vq/module.py:45-48) and weight_norm(nn.Conv1d)
@@ -39,14 +43,14 @@ int bc_abi_version(void);
  * bc_snake_fwd).  W is the FOLDED weight g*v/||v|| [Cout][Cin][K] packed by bc_conv1d_pack for
  * cfg = bc_conv1d_select_cfg(Cout, Cin, K, stride, dilation, mode) (any other valid tile id also
  * runs — tuning — with weights packed for that same cfg; a tile the shape does not fit returns 3).
- * mode 0: fp32 MFMA (v_mfma_f32_16x16x4_f32).  mode 1: fp32-accurate "x6" MFMA — both operands
+ * mode 0: fp32 MFMA (v_mfma_f32_16x16x4_f32).  mode 1 (the package default): fp32-accurate "x6" MFMA — both operands
  * split exactly into three bf16 terms, six bf16 products per pair accumulated in fp32 — for the
  * shapes where it applies (Cin >= 16), else the fp32 kernel.  Its error against fp64 is at or below
  * the fp32 kernel's.  mode 2: plain bf16 products with fp32 accumulation (one MFMA
  * per pair; BASELINE config 5's "bf16 encoder conv stack"; activations stay fp32 in memory) where
  * Cin >= 16, else fp32.  bc_reslstm_fwd runs mode 2 as mode 3 (the recurrence stays fp32-class; its
  * input projection is packed with cfg = bc_conv1d_select_cfg(..., 3)).
- * mode 3 ("h3", the package default): fp32-class block-scaled 2 x fp16 split — each operand block is
+ * mode 3 ("h3", opt-in; 22-bit operands, narrower than the reference's fp32): block-scaled 2 x fp16 split — each operand block is
  * scaled by a power of two from its maximum (weights per output row, packed by bc_conv1d_pack;
  * activations per staged 32-channel chunk) and split v*S = hi + lo (two fp16 terms, 22 significant
  * bits); a*b accumulates hi*hi + hi*lo + lo*hi in fp32 on v_mfma_f32_16x16x32_f16 (the dropped lo*lo

@@ -20,10 +20,10 @@ def test_kernel_peak_by_operand_planes():
         assert abs(got - peak) < 1e-9, (name, got, peak)
 
 
-def test_committed_pmc_summaries_are_readable():
+def test_committed_pmc_summaries_are_readable(tmp_path):
     """bench.py reads the newest profiles/*pmc_traffic.json for the roofline's `traffic`: every committed summary has
-    the tools/pmc_summary.py layout ({"kernels": {name: {"traffic_bytes_corrected", ...}}}), and the dominant h3
-    kernel resolves to a positive per-launch byte count."""
+    the tools/pmc_summary.py layout ({"kernels": {name: {"traffic_bytes_corrected", ...}}}); a summary is used only
+    when its `lib_digest` is the running library's (bc_build_digest), never for other kernel code."""
     import glob
     import json
     import os
@@ -35,5 +35,10 @@ def test_committed_pmc_summaries_are_readable():
         assert isinstance(d.get("kernels"), dict), f
         for name, v in d["kernels"].items():
             assert "traffic_bytes_corrected" in v, (f, name)
-    traffic, util, src = bench.pmc_traffic("conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, true>")
-    assert traffic and traffic > 0 and src == os.path.basename(files[-1])
+    k = "conv1d_x6_kernel<6, 2, 2, 8, 3, false, 1, false, true>"
+    for i, dig in enumerate(("a" * 64, "b" * 64)):
+        (tmp_path / f"r0{i}_pmc_traffic.json").write_text(json.dumps(
+            {"lib_digest": dig, "kernels": {k: {"traffic_bytes_corrected": 100.0 + i, "mfma_util": 0.5}}}))
+    assert bench.pmc_traffic(k, running="a" * 64, profiles=str(tmp_path)) == (100.0, 0.5, "r00_pmc_traffic.json")
+    assert bench.pmc_traffic(k, running="b" * 64, profiles=str(tmp_path))[0] == 101.0
+    assert bench.pmc_traffic(k, running="c" * 64, profiles=str(tmp_path)) == (None, None, None)

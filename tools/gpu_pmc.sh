@@ -6,7 +6,7 @@ set -u
 D=${PMC_DIR:-gpurun_out/pmc}
 mkdir -p $D
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timer --no-x6}
+ARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timer --no-h3}
 PASSES=${PMC_PASSES:-"FETCH_SIZE WRITE_SIZE MFMA"}
 for pass in $PASSES; do
   ctr=$pass

@@ -57,7 +57,11 @@ def main():
             d["mfma_util"] = mean(util)
             d["mfma_busy_cycles"] = mean(busy[k])
         res[k] = d
-    out = {"note": "per-launch averages; traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 wide-read correction); "
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from audiotokenization_amd import build_lib
+
+    out = {"lib_digest": build_lib.lib_digest(build_lib.LIB),  # bench.py reports this traffic only on that library
+           "note": "per-launch averages; traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 wide-read correction); "
                    "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
            "kernels": res}
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
