@@ -297,7 +297,7 @@ int bc_lstm_pack_hh(const float* w_hh_host, float* packed_host, int H, int mode)
 
 // workspace: status [64 floats: int32 timeout count of this call] | xt [H][T*B] | gx [4H][T*B] |
 // y0 [H][T*B] | y1 [H][T*B] | c [H][B] | hfrag x2 or the persistent kernel's region | the input projection's
-// pre-split B planes (pw_presplit.hip, h3)
+// pre-split B planes (pw_presplit.hip, h3 and x6)
 constexpr long long LSTM_WS_STATUS_FLOATS = 64;
 static long long lstm_frag_floats(int B, int H) { return (long long)((B + 63) / 64) * 64 * H; }
 static long long lstm_ws_head_floats(int B, int H, int T) {
@@ -306,7 +306,7 @@ static long long lstm_ws_head_floats(int B, int H, int T) {
   const long long seq = lstm_seq_ok(H) ? lstm_seq_workspace_bytes(H, T) / 4 : 0;
   return (LSTM_WS_STATUS_FLOATS + tb * H * 3 + tb * 4 * H + (long long)H * B + (frag > seq ? frag : seq) + 3) / 4 * 4;
 }
-// The input projection on the pre-split GEMM (h3, Cout % 192 == 0, Cin % 32 == 0): on by default; BC_LSTM_PRESPLIT=0
+// The input projection on the pre-split GEMM (h3 and x6, Cout % 192 == 0, Cin % 32 == 0): on by default; BC_LSTM_PRESPLIT=0
 // or bc_debug_set_lstm_presplit(0) runs it on conv1d_x6_kernel (A/B timing, the bit-identity test).
 static int g_lstm_presplit = [] {
   const char* e = getenv("BC_LSTM_PRESPLIT");
@@ -363,8 +363,11 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   int rc;
   // (few columns, e.g. a streaming chunk: presplit_b walks every chunk of a 256-column tile in one workgroup, a fixed
   // ~220 us, so below 32 tiles the plain 322 launch, bit-identical, is faster; profiles/r04v_presplit_narrow.txt)
-  if (psplit && g_lstm_presplit && cfg == 322 && (tb >= 32 * 256 || g_lstm_presplit == 2) && pw_presplit_ok(4 * H, Cin, tb))
+  const bool ps_size = tb >= 32 * 256 || g_lstm_presplit == 2;
+  if (psplit && g_lstm_presplit && cfg == 322 && ps_size && pw_presplit_ok(4 * H, Cin, tb))
     rc = pw_presplit_launch(a, psplit, st);  // same planes, scales and MFMA chains as cfg 322: bit-identical
+  else if (psplit && g_lstm_presplit && cfg == 122 && ps_size && pw_presplit_x6_ok(4 * H, Cin, tb))
+    rc = pw_presplit_x6_launch(a, psplit, st);  // x6: the same planes and chains as cfg 122, 128-row tiles
   else
     rc = conv_launch(a, 1, cfg, st);
   if (rc) return rc;

@@ -63,6 +63,8 @@ int convT_interleave_launch(const float* ph, const float* ph2, float* y, float* 
 long long pw_presplit_bytes(int Cin, long long N);
 bool pw_presplit_ok(int Cout, int Cin, long long N);
 int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st);
+bool pw_presplit_x6_ok(int Cout, int Cin, long long N);  // the x6 variant (128 x 256 tile over cfg-322 weights)
+int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,

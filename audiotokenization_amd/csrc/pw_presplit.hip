@@ -225,9 +225,209 @@ __global__ void __launch_bounds__(1024, 1) pw_presplit_kernel(ConvArgs a, const 
   conv_epilogue<MT, NT, true>(a, acc, 0, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
 }
 
+// ------------------------------------------------------------------------------------------------
+// x6 (P = 3): the same idea without block scales (the 3 x bf16 split is exact per element).  Three planes of a
+// 256-column chunk are 48 KiB, so the 192-row GEMM's A + B double buffers (2 x 36 + 2 x 48 KiB) would exceed the
+// 160 KiB LDS: the x6 GEMM tile is 128 rows x 256 columns (16 waves of 64 x 32, 4 x 2 MFMA tiles each), A and B
+// double-buffered (2 x 24 + 2 x 48 = 144 KiB).  A comes from the weights packed for cfg 322 (192-row groups): its
+// 1-KiB pieces are per (16-row m-tile, plane, chunk), so any 16-row-aligned tile gathers them piece by piece.
+// Per output the same chunk order and the same six-MFMA chain as conv1d_x6_kernel<..., P = 3>: bit-identical to
+// the cfg-322 x6 launch (tests/test_gpu_kernels.py::test_lstm_projection_presplit_bit_identical[x6]).
+constexpr int PX_MT = 4, PX_NT = 2, PX_WM = 2, PX_WN = 8;
+constexpr int PX_BM = 16 * PX_MT * PX_WM;  // 128
+constexpr int PX_QA = PX_WM * PX_MT;       // 8 m-tiles
+constexpr int PX_APIECES = 3 * PX_QA;      // 24 pieces of a chunk's A block
+constexpr int PX_BPIECES = 3 * PS_PLANE / 1024;  // 48 pieces of a chunk's B block (3 per wave)
+constexpr int PX_LDS = 2 * 3 * PS_PLANE + 2 * PX_APIECES * 1024;  // 144 KiB
+constexpr int P322_QA = 12;                // m-tiles per 192-row group of the cfg-322 packing
+
+__global__ void __launch_bounds__(256) presplit_b_x6_kernel(const float* __restrict__ x, unsigned char* __restrict__ planes,
+                                                            int Cin, int N, int nch) {
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = j * PS_BN + 4 * lane;
+  auto load = [&](int c, float (&v)[8][4]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ch = c * X6_BKC + 8 * w + k;
+      const float* row = x + (long long)ch * N;
+      if (ch < Cin && n + 3 < N && (N & 3) == 0) {
+        const floatx4 q = *reinterpret_cast<const floatx4*>(row + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[k][r] = q[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[k][r] = (ch < Cin && n + r < N) ? row[n + r] : 0.f;
+      }
+    }
+  };
+  auto body = [&](int c, const float (&v)[8][4]) {
+    unsigned char* pb = planes + ((long long)j * nch + c) * (3 * PS_PLANE);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = 4 * lane + r;
+      unsigned h[4], m[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) split2(v[2 * k][r], v[2 * k + 1][r], h[k], m[k], l[k]);
+      const int off = col * 64 + 16 * (w ^ ((col >> 1) & 3));
+      *reinterpret_cast<u32x4_t*>(pb + off) = (u32x4_t){h[0], h[1], h[2], h[3]};
+      *reinterpret_cast<u32x4_t*>(pb + PS_PLANE + off) = (u32x4_t){m[0], m[1], m[2], m[3]};
+      *reinterpret_cast<u32x4_t*>(pb + 2 * PS_PLANE + off) = (u32x4_t){l[0], l[1], l[2], l[3]};
+    }
+  };
+  float va[8][4], vb[8][4];
+  if (nch > 0) load(0, va);
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) load(c + 1, vb);
+    body(c, va);
+    if (c + 1 < nch) {
+      if (c + 2 < nch) load(c + 2, va);
+      body(c + 1, vb);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024, 1) pw_presplit_x6_kernel(ConvArgs a, const unsigned char* __restrict__ planes) {
+  constexpr int MT = PX_MT, NT = PX_NT, WM = PX_WM, NW = PX_WM * PX_WN;
+  typedef bf16x8_t frag_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_px[];
+  unsigned char* Bs = smem_px;                        // [2][3 planes][PS_PLANE]
+  unsigned char* As = smem_px + 2 * 3 * PS_PLANE;     // [2][3 planes][QA][1 KiB]
+
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int mt_idx = wg % a.ntm;
+  const int nt_idx = wg / a.ntm;
+  const int m0 = mt_idx * PX_BM;
+  const int n0 = nt_idx * PS_BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int nch = a.nchunks;
+
+  const unsigned char* wbase = reinterpret_cast<const unsigned char*>(a.w);
+  const unsigned char* bblk = planes + (long long)nt_idx * nch * (3 * PS_PLANE);
+  // A piece q = plane * QA + local m-tile: m-tile g = m0 / 16 + local of the cfg-322 packing
+  // [group g / 12][chunk][plane][g % 12][1 KiB]
+  auto issue_a = [&](int c) {
+    unsigned char* da = As + (c & 1) * (PX_APIECES * 1024);
+    for (int q = wave; q < PX_APIECES; q += NW) {
+      const int p = q / PX_QA, g = m0 / 16 + q % PX_QA;
+      const unsigned char* src =
+          wbase + ((((long long)(g / P322_QA) * nch + c) * 3 + p) * P322_QA + g % P322_QA) * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (lds_void_t)(da + q * 1024), 16, 0, 0);
+    }
+  };
+  auto issue_b = [&](int c) {
+    const unsigned char* sb = bblk + (long long)c * (3 * PS_PLANE);
+    unsigned char* db = Bs + (c & 1) * (3 * PS_PLANE);
+#pragma unroll
+    for (int k = 0; k < PX_BPIECES / NW; ++k) {
+      const int q = wave + k * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(sb + q * 1024 + lane * 16), (lds_void_t)(db + q * 1024), 16, 0, 0);
+    }
+  };
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int col_lane = wn * NT * 16 + (lane & 15);
+  const int bgo = col_lane * 64 + 16 * ((lane >> 4) ^ ((col_lane >> 1) & 3));  // conv1d_x6_kernel's bgrp
+  auto compute = [&](int c) {
+    const unsigned char* Ab = As + (c & 1) * (PX_APIECES * 1024);
+    const unsigned char* Bcol = Bs + (c & 1) * (3 * PS_PLANE) + bgo;
+    frag_t bf[NT][3];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bf[j][p] = *reinterpret_cast<const frag_t*>(Bcol + j * 16 * 64 + p * PS_PLANE);
+    frag_t af[2][3];
+    auto load_a = [&](int i, frag_t (&d)[3]) {
+      const unsigned char* Aq = Ab + (wm * MT + i) * 1024 + lane * 16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const frag_t*>(Aq + p * PX_QA * 1024);
+    };
+    load_a(0, af[0]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      const frag_t a0 = af[i & 1][0], a1 = af[i & 1][1], a2 = af[i & 1][2];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        if (j == 1 && i + 1 < MT) {
+          __builtin_amdgcn_sched_barrier(0);
+          load_a(i + 1, af[(i + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // conv1d_x6_kernel<..., P = 3>'s chain, in its order
+        floatx4 t = acc[i][j];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][2], a0, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
+        acc[i][j] = t;
+      }
+    }
+  };
+
+  // step c: A(c + 1) and B(c + 1) into the buffers chunk c - 1 used (freed by step c - 1's barrier), compute chunk
+  // c, wait for this wave's copies, barrier (every wave's copies have landed, every wave is done with buffer c & 1)
+  issue_a(0);
+  dma_issue_order();
+  issue_b(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) {
+      issue_a(c + 1);
+      dma_issue_order();
+      issue_b(c + 1);
+      dma_issue_order();
+    }
+    compute(c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  }
+  conv_epilogue<MT, NT>(a, acc, 0, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
+}
+
 long long pw_presplit_bytes(int Cin, long long N) {
+  // the larger of the two layouts: x6's three planes (no scales) >= h3's two planes + one scale per chunk
   const long long ntn = (N + PS_BN - 1) / PS_BN, nch = (Cin + X6_BKC - 1) / X6_BKC;
-  return ntn * nch * (2LL * PS_PLANE + 4);
+  const long long h3 = ntn * nch * (2LL * PS_PLANE + 4), x6 = ntn * nch * 3LL * PS_PLANE;
+  return h3 > x6 ? h3 : x6;
+}
+
+bool pw_presplit_x6_ok(int Cout, int Cin, long long N) {
+  return Cout % PX_BM == 0 && Cout % (16 * P322_QA) == 0 && Cin % X6_BKC == 0 && N > 0 && N <= 0x7fffffffLL &&
+         (long long)Cin * N * 4 <= 0x7fffffffffffLL;
+}
+
+// a: the pointwise conv as conv_launch would run it on cfg 322 in x6 (K = 1, stride 1, one batch item, x [Cin][N],
+// y [Cout][N]); w packed for cfg 322 (P = 3).  ws: pw_presplit_bytes(Cin, N) bytes (the three planes).
+int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st) {
+  if (a.K != 1 || a.s != 1 || a.d != 1 || a.pl != 0 || a.ps || !ws) return BC_ERR_ARG;
+  if (!pw_presplit_x6_ok(a.Cout, a.Cin, a.Nout) || a.Tin != a.Nout) return BC_ERR_UNSUPPORTED;
+  const long long N = a.Nout;
+  const int ntn = (int)((N + PS_BN - 1) / PS_BN), nch = a.Cin / X6_BKC;
+  unsigned char* planes = reinterpret_cast<unsigned char*>(ws);
+  hipLaunchKernelGGL(presplit_b_x6_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, a.Cin, (int)N, nch);
+  BC_CHECK_LAUNCH();
+  a.vec = conv_epilogue_vec_ok(a);
+  a.ntm = a.Cout / PX_BM;
+  a.ntn = ntn;
+  a.nchunks = nch;
+  const long long nwg = (long long)a.ntm * ntn;
+  if (nwg > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  a.nwg = (int)nwg;
+  a.wsc = nullptr;
+  hipLaunchKernelGGL(pw_presplit_x6_kernel, dim3(a.nwg), dim3(1024), PX_LDS, st, a, planes);
+  BC_CHECK_LAUNCH();
+  return BC_OK;
 }
 
 bool pw_presplit_ok(int Cout, int Cin, long long N) {

@@ -299,14 +299,16 @@ def test_reslstm(dev, H, layers, B, T, prec):
     assert L.load().bc_lstm_status(1) == 0
 
 
+@pytest.mark.parametrize("prec", ["h3", "x6"])
 @pytest.mark.parametrize("H,B,T", [(1536, 3, 100), (768, 2, 700), (1536, 64, 40), (768, 3, 33)])
-def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
-    """h3: the ResLSTM input projection on the pre-split GEMM (pw_presplit.hip: B planes and block scales made once
-    per 256-column tile, copied by LDS-DMA) against the same projection on conv1d_x6_kernel cfg 322: the same
-    blocks, scales and MFMA chains, so the layer outputs are bit-identical; T * B not a multiple of 256 (ragged last
-    column tile) and not a multiple of 4 (no 16-byte rows) included; and within the oracle's tolerance."""
+def test_lstm_projection_presplit_bit_identical(dev, H, B, T, prec):
+    """The ResLSTM input projection on the pre-split GEMM (pw_presplit.hip: B planes (and, h3, block scales) made once
+    per 256-column tile, copied by LDS-DMA; x6 on 128-row tiles over the cfg-122 weights) against the same projection
+    on conv1d_x6_kernel cfg 322 / 122: the same blocks, scales and MFMA chains, so the layer outputs are
+    bit-identical; T * B not a multiple of 256 (ragged last column tile) and not a multiple of 4 (no 16-byte rows)
+    included; and within the oracle's tolerance."""
     old = L.precision_mode()
-    L.set_precision("h3")
+    L.set_precision(prec)
     lib = L.load()
     try:
         g = torch.Generator().manual_seed(H * 3 + B + T)
@@ -328,7 +330,7 @@ def test_lstm_projection_presplit_bit_identical(dev, H, B, T):
         L._mode = old
     assert torch.equal(y_ps, y_x6), (y_ps - y_x6).abs().max()
     want = O.res_lstm(x, sd, "", 2)
-    assert_close_rel(y_ps, want, 2e-5, f"lstm h3 presplit H={H}")
+    assert_close_rel(y_ps, want, 2e-5, f"lstm {prec} presplit H={H}")
 
 
 @pytest.mark.parametrize("lprec", ["h3", "x6"])
