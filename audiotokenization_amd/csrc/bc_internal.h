@@ -41,6 +41,11 @@ bool x6_cfg_valid(int cfg);
 long long x6_packed_bytes(int Cout, int Cin, int K, int cfg);
 void x6_pack_weight(const float* w, unsigned short* out, int Cout, int Cin, int K, int cfg);
 int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st);
+// x6 convs with register-resident weight fragments on the 8-wave 192 x 256 tile (conv1d_x6ra.hip): the launches
+// x6_launch routes from cfg 120 (the multi-tap stride-1 convs incl. the phase-decomposed strided ones)
+bool x6ra_applies(int K, int s, int d, int ps);
+const char* x6ra_kernel_name(bool b4);
+int x6ra_launch(ConvArgs& a, int B, hipStream_t st);
 int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n);
 int conv_kernel_name(int cfg_id, int K, int s, int d, char* buf, int n);
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n);

@@ -182,17 +182,32 @@ static int h3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
 // input projection 8.99 -> 7.89, phase-decomposed stride 2 96 -> 192 / 192 -> 384 4.86 / 8.05 -> 3.97 / 6.44, stride 5
 // 768 -> 1536 10.79 -> 8.96 -- except the stride-5 384 -> 768 (phase-decomposed 256 x 256: 13.58 -> 10.94) and the final
 // k3 1536 -> 1024 (256 x 256: 4.02 -> 3.59); 48 -> 96 stride 2 keeps the 96-row tile (2109: 3.16 vs 4.89).
+// BC_X6_RA (bits; default 2): the register-A kernel (conv1d_x6ra.hip, x6 on the 8-wave 192 x 256 tile = cfg 120) for
+// 1: the multi-tap stride-1 convs with Cout % 192 == 0, 2: the phase-decomposed stride >= 3 ones, in place of the
+// 16-wave tile 122 (same packing, bit-identical outputs).  Measured (profiles/r05g_ra.txt, B = 64): stride 5 384 -> 768
+// 10.61 -> 10.46 ms, 768 -> 1536 8.67 -> 8.38; the k7 convs 8.55 -> 9.08 (C = 192 d9), 15.66 -> 16.06 (384), 12.28 ->
+// 12.19 (768) and the stride-2 phase convs 6.36 -> 6.91, 4.05 -> 4.66 stay on 122.
+static int x6_ra() {
+  static const int v = [] {
+    const char* e = getenv("BC_X6_RA");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 static int x6p3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   (void)Cin;
   auto fits = [&](int tile, int K_, int s_, int d_) { return x6_ncol(kX6Tiles[tile], K_, s_, d_) <= 32 * X6_MAXCOL_ITERS; };
+  const int ra1 = (x6_ra() & 1) ? 120 : 122, ra2 = (x6_ra() & 2) ? 120 : 122;
+  if (s == 1 && K > 1 && Cout % 192 == 0 && fits(22, K, 1, d)) return ra1;
   if (s == 1 && Cout % 192 == 0 && fits(22, K, 1, d)) return 122;
   if (s == 1 && K > 1 && Cout % 256 == 0 && fits(21, K, 1, d)) return 121;
   const int Kp = (K + s - 1) / s;
   if (s == 2 && d == 1 && Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 2000 + 122;
   if (s >= 3 && s <= 16 && d == 1) {
-    if (Cout % 192 == 0 && Cout >= 1536 && fits(22, Kp, 1, 1)) return 1000 * s + 122;
+    if (Cout % 192 == 0 && Cout >= 1536 && fits(22, Kp, 1, 1)) return 1000 * s + (Kp > 1 ? ra2 : 122);
     if (Cout % 256 == 0 && fits(21, Kp, 1, 1)) return 1000 * s + 121;
-    if (Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 1000 * s + 122;
+    if (Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 1000 * s + (Kp > 1 ? ra2 : 122);
   }
   return -1;
 }
@@ -259,7 +274,8 @@ int x6_narrow_cfg(int cfg, int Cout, int K, int s, int d, int planes, int B, int
     if (Tout > 64 || Cout % 128 != 0) return cfg;  // columns (k3 1536 -> 1024: 0.377 -> 0.176 ms at 16 x 6 columns,
     tile = 17;                                      // 0.411 -> 0.245 at 64 x 24; profiles/r04y_k3_sweep.txt)
   } else {
-    if (cfg - base != 122) return cfg;
+    // (x6: the register-A tile 120 narrows like 122; h3's block scales follow the tile, so its 320 stays)
+    if (cfg - base != 122 && !(planes == 3 && cfg - base == 120)) return cfg;
     auto nwg = [&](int bm) { return (long long)((Cout + bm - 1) / bm) * B; };
     const bool fill192 = Cout % 192 == 0 && nwg(192) >= cus;
     if (Tout <= 64) tile = fill192 ? 15 : (Cout % 96 == 0 ? 16 : 12);
@@ -416,6 +432,8 @@ int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n) {
   }
   const X6Tile& t = cfg_tile(cfg);
   const int P = cfg_planes(cfg);
+  if (P == 3 && cfg_base(cfg) == 120 && x6ra_applies(K, s, d, cfg_phase(cfg)))  // x6_launch's routing
+    return snprintf(buf, n, "%s", x6ra_kernel_name(cfg_phase(cfg) == 0));
   const X6Variant v = x6_variant(t, P, K, s, d, cfg_phase(cfg));
   // (the 16-byte staging also needs Tin % 4 == 0 and 16-B aligned rows at launch, x6_b4_fits: true of every
   // BigCodec shape at the configs' clip lengths; a launch that fails it runs the single-float variant)
@@ -442,6 +460,7 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
     cfg = cfg_base(cfg);
   }
   const int tile = cfg_base(cfg) % 100;
+  if (cfg_planes(cfg) == 3 && tile == 20 && x6ra_applies(a.K, a.s, a.d, a.ps)) return x6ra_launch(a, B, st);
   switch (cfg_planes(cfg)) {
     case 1: return x6_launch_tile<1>(a, B, tile, st);
     case 2: return x6_launch_tile<2>(a, B, tile, st);

@@ -46,7 +46,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
     for (int j = 0; j < NT; ++j) {
       const int nb = col0 + j * 16 + (lane >> 4) * 4;
       d[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (rb && vec_tile(co, nb) && BC_DOK((long long)co * a.yT + a.ooff + nb + 3 < a.rbs))
+      if (rb && vec_tile(co, nb) && BC_DOK(co >= 0 && nb >= 0 && (long long)co * a.yT + a.ooff + nb + 3 < a.rbs))
         d[j] = *reinterpret_cast<const floatx4*>(rb + (long long)co * a.yT + a.ooff + nb);
     }
   };
@@ -67,7 +67,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
       if (nb >= a.Nout) continue;
       if (vec_tile(co, nb)) {
         const long long yi = rowoff + nb;
-        if (!BC_DOK(yi + 3 < a.ybs)) continue;  // debug build: the tile's 16 bytes must lie inside the batch item
+        if (!BC_DOK(yi >= 0 && yi + 3 < a.ybs)) continue;  // debug build: the tile's 16 bytes inside the batch item
         const floatx4 r = (MT == 1 && RP) ? rpre[j] : rr[i & 1][j];
         floatx4 v, sv;
 #pragma unroll
@@ -92,7 +92,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
           const int n = nb + q;
           if (n >= a.Nout) break;
           const long long yi = rowoff + (long long)n * a.ostride;
-          if (!BC_DOK(yi < a.ybs && (!rb || yi < a.rbs))) break;
+          if (!BC_DOK(yi >= 0 && yi < a.ybs && (!rb || yi < a.rbs))) break;
           const float v =
               conv_epi_value(a, SC ? acc[i][j][q] * sc : acc[i][j][q], bias, rb ? rb[yi] : 0.f, rb != nullptr);
           if (snk) {

@@ -11,6 +11,7 @@
 //  transpose kernels: [B][C][T] <-> [C][T][B] layouts around the ResLSTM (vq/module.py:160-166).
 //  synth_clips      : counter-hash white noise generated in HBM.
 //  stream_window    : a causal stream's [carried context | chunk] window (+ Snake) and its next context.
+#include <algorithm>
 #include "bc_common.h"
 #include "bc_internal.h"
 
@@ -194,26 +195,29 @@ int snake_launch(const float* x, const float* sa, const float* sb, float* y, int
 // epilogue) or the identity; a missing ctx reads zeros (a stream's first chunk: the causal conv's zero padding,
 // and snake(0) = 0, so zeros are the same before and after the activation).  x may be a strided view (row pitch
 // xT, batch pitch xbs): a ResidualUnit run over its own window hands its last n columns on without a copy.
+// 2-D grid (three 64-bit divisions per element): y walks the (b, c) rows (one 32-bit division per row),
+// x the W = P + n window columns of a row
 __global__ void __launch_bounds__(256) stream_window_kernel(const float* __restrict__ x, long long xbs, long long xT,
                                                             const float* __restrict__ ctx, const float* __restrict__ sa,
                                                             const float* __restrict__ sb, float* __restrict__ win,
-                                                            float* __restrict__ ctx_out, int C, int n, int P,
-                                                            long long total) {
-  const long long W = (long long)P + n;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const long long row = i / W, j = i - row * W;
-    const int c = (int)(row % C);
-    const long long b = row / C;
-    float v;
-    if (j < P) {
-      v = ctx ? ctx[row * P + j] : 0.f;
-    } else {
-      v = x[b * xbs + c * xT + (j - P)];
-      if (sa) v = snake(v, sa[c], sb[c]);
+                                                            float* __restrict__ ctx_out, int C, int n, int P, int rows) {
+  const int W = P + n;
+  for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+    const int b = row / C, c = row - b * C;
+    const float* xr = x + (long long)b * xbs + (long long)c * xT;
+    float* wr = win + (long long)row * W;
+    const float a_ = sa ? sa[c] : 0.f, b_ = sa ? sb[c] : 0.f;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < W; j += gridDim.x * blockDim.x) {
+      float v;
+      if (j < P) {
+        v = ctx ? ctx[(long long)row * P + j] : 0.f;
+      } else {
+        v = xr[j - P];
+        if (sa) v = snake(v, a_, b_);
+      }
+      wr[j] = v;
+      if (j >= n) ctx_out[(long long)row * P + (j - n)] = v;
     }
-    win[i] = v;
-    if (j >= n) ctx_out[row * P + (j - n)] = v;
   }
 }
 
@@ -221,10 +225,12 @@ int stream_window_launch(const float* x, long long xbs, long long xT, const floa
                          float* win, float* ctx_out, int B, int C, int n, int P, hipStream_t st) {
   if (!x || !win || B < 0 || C < 1 || n < 1 || P < 0 || xT < n || xbs < (long long)(C - 1) * xT + n) return BC_ERR_ARG;
   if ((sa == nullptr) != (sb == nullptr) || (P > 0 && !ctx_out)) return BC_ERR_ARG;
-  const long long total = (long long)B * C * ((long long)P + n);
-  if (total == 0) return BC_OK;
-  hipLaunchKernelGGL(stream_window_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, xbs, xT, ctx, sa, sb, win,
-                     ctx_out, C, n, P, total);
+  const long long rows = (long long)B * C, W = (long long)P + n;
+  if (rows == 0) return BC_OK;
+  if (rows > 0x7fffffffLL || W > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
+  const int gx = (int)std::min<long long>((W + 255) / 256, 1024), gy = (int)std::min<long long>(rows, 65535);
+  hipLaunchKernelGGL(stream_window_kernel, dim3(gx, gy), dim3(256), 0, st, x, xbs, xT, ctx, sa, sb, win, ctx_out, C, n,
+                     P, (int)rows);
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

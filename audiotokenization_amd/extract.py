@@ -241,6 +241,9 @@ class _SinkWriter:
         self.t.join()
 
 
+_CONTROL_GROUPS = {}  # (world group, ranks) -> the gloo control group of ShardedExtractor (one per process)
+
+
 class ShardedExtractor:
     """Clip-sharded extraction of clips [0, n_clips) over `world` ranks.
 
@@ -287,15 +290,21 @@ class ShardedExtractor:
 
     def _control_group(self):
         """The host-side group of the status exchange: the device group itself when it is gloo, else a gloo
-        group over the same ranks (every rank constructs the extractor, so every rank creates it)."""
+        group over the same ranks, created ONCE per process and set of ranks and shared by every extractor (ADVICE
+        r04: one new group per extractor was never destroyed, and every rank had to build extractors in the same
+        order).  new_group is collective, so the first extractor over a set of ranks is built on every rank."""
         import torch.distributed as dist
 
         if not dist.is_available() or not dist.is_initialized():
             return None
         if dist.get_backend(self.group) == "gloo":
             return self.group
-        ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
-        return dist.new_group(ranks=ranks, backend="gloo")
+        ranks = tuple(dist.get_process_group_ranks(self.group)) if self.group is not None else None
+        key = (id(dist.group.WORLD), ranks)
+        grp = _CONTROL_GROUPS.get(key)
+        if grp is None:
+            grp = _CONTROL_GROUPS[key] = dist.new_group(ranks=list(ranks) if ranks else None, backend="gloo")
+        return grp
 
     def step(self, bi: int):
         """Queue batch `bi` of every rank on the device, then finish the batches beyond the pipeline depth.

@@ -60,6 +60,14 @@ class StreamingEncoder:
         self._ctx: Dict[int, torch.Tensor] = {}
         self._lstm: Dict[int, tuple] = {}
         self.samples = 0
+        # the precision the carried state belongs to: the fused and the two-launch ResidualUnit paths keep different
+        # context (raw input vs activated input), and which one runs depends on the mode (ADVICE r04)
+        self._mode = _lib.precision_mode()
+
+    def _check_mode(self):
+        if _lib.precision_mode() != self._mode:
+            raise RuntimeError(f"precision changed mid-stream ({self._mode} -> {_lib.precision_mode()}): the carried "
+                               "context belongs to the old mode; reset() the stream first")
 
     def _window(self, key, x, P: int, act=None):
         """[carried context | x] (B, C, P + n), `act` (a Snake Activation1d or None) applied to x, as the input of a
@@ -100,6 +108,7 @@ class StreamingEncoder:
         return y
 
     def push(self, x) -> torch.Tensor:
+        self._check_mode()
         with _lib.status_scope():
             return self._push(x)
 
@@ -169,6 +178,7 @@ class StreamingDecoder(StreamingEncoder):
         return out[0]
 
     def push(self, z) -> torch.Tensor:
+        self._check_mode()
         with _lib.status_scope():
             return self._push_dec(z)
 

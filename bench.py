@@ -64,6 +64,8 @@ def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
     planes = targs[4] if kname.startswith(("conv1d_x6_kernel", "resunit_x6_kernel")) and len(targs) >= 5 else None
+    if kname.startswith("conv1d_x6ra_kernel"):  # conv1d_x6ra.hip: x6 (three bf16 planes) only
+        planes = "3"
     if kname.startswith(("resunit_rr_kernel", "resunit_strip_kernel")):  # resunit_rr.hip: h3 (two fp16 planes) only
         planes = "2"
     if planes == "1":
@@ -92,7 +94,7 @@ def kernel_table(summ, steps, probe, n=8):
         rows.append({"kernel": name, "launches_per_step": d["launches"] // steps,
                      "ms_per_step": round(d["ms_total"] / steps, 3), "tflops": round(tf, 1),
                      "frac_mfma_spec": round(tf / peak, 3),
-                     "frac_mfma_probe": round(tf * mult / probe, 3) if name.startswith(("conv1d_x6", "resunit_")) else None,
+                     "frac_mfma_probe": round(tf * mult / probe, 3) if name.startswith(("conv1d_x6", "resunit_", "pw_presplit")) else None,
                      "gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 3)})
     return rows
 
@@ -107,7 +109,7 @@ def roofline(summ, steps, probe):
     conv_ms = sum(v["ms_total"] for v in summ.values())
     traffic, mutil, tsrc = pmc_traffic(kname)
     peak, mult, note = kernel_peak(kname)
-    practical = probe / mult if kname.startswith("conv1d_x6_kernel") else None
+    practical = probe / mult if kname.startswith(("conv1d_x6_kernel", "conv1d_x6ra_kernel")) else None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "peak_note": note,
             "probe_bf16_tflops": round(probe, 1),

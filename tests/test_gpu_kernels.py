@@ -100,7 +100,8 @@ def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
     phase-decomposed strided convs as 1000 s + tile) stages the same B chunks with the same block scales
     and runs the same per-output MFMA chains: bit-identical outputs, and within the conv tolerance of the
     oracle.  The bf16 planes (cfg - 100) and the x6 planes (cfg - 200: three bf16 planes, the 16-wave tile
-    without the A-fragment prefetch) run the same two tiles."""
+    without the A-fragment prefetch) run the same two tiles; in x6 the 8-wave tile (120) is the register-A kernel
+    (conv1d_x6ra.hip), bit-identical to the 16-wave one."""
     old = L.precision_mode()
     L.set_precision(tprec)
     if tprec != "h3":
@@ -135,12 +136,16 @@ def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
 
 
 @pytest.mark.parametrize("Cin,Cout,d,B,T,cfgs", [(192, 192, 3, 2, 70000, (322, 320)), (384, 384, 9, 3, 24000, (322, 320)),
-                                             (768, 768, 9, 3, 8000, (322, 321)), (192, 192, 1, 2, 70000, (222, 220))])
+                                             (768, 768, 9, 3, 8000, (322, 321)), (192, 192, 1, 2, 70000, (222, 220)),
+                                             (192, 192, 9, 2, 70000, (122, 120)), (384, 384, 3, 3, 24001, (122, 120)),
+                                             (768, 768, 1, 3, 8000, (122, 120))])
 def test_k7_tiles_large(dev, Cin, Cout, d, B, T, cfgs):
     """k7 convs at encoder scale (hundreds of tiles, several per CU): two tiles (16 waves and 8 waves, each a
     different grid and tile walk) agree bit for bit, and the output matches the fp64 oracle in windows at the
-    start, across tile boundaries and at the end."""
-    prec = "bf16" if cfgs[0] < 300 else "h3"
+    start, across tile boundaries and at the end.  x6 (cfg 1xx): the 8-wave 192 x 256 tile is the register-A kernel
+    (conv1d_x6ra.hip: weight fragments streamed into registers, the B tile double-buffered; T = 24001 runs its
+    single-float staging)."""
+    prec = {1: "x6", 2: "bf16", 3: "h3"}[cfgs[0] // 100]
     old = L.precision_mode()
     L.set_precision(prec)
     try:
@@ -165,7 +170,7 @@ def test_k7_tiles_large(dev, Cin, Cout, d, B, T, cfgs):
         L._mode = old
     assert torch.equal(outs[cfgs[0]], outs[cfgs[1]]), (outs[cfgs[0]] - outs[cfgs[1]]).abs().max()
     got = outs[cfgs[0]]
-    tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if prec == "h3" else 2e-2
+    tol = 3e-6 * max(1.0, np.sqrt(Cin * K / 64)) if prec != "bf16" else 2e-2
     xp = torch.nn.functional.pad(x.double(), (pad, pad))
     sd64 = {k: v.double() for k, v in sd.items()}
     W = 300
@@ -890,7 +895,8 @@ def test_narrow_launch_tile(dev, Cin, Cout, K, d, B, T, prec):
         lib = L.load()
         wide = lib.bc_conv1d_select_cfg(Cout, Cin, K, 1, d, L.precision_mode())
         narrow = lib.bc_conv1d_select_cfg_n(Cout, Cin, K, 1, d, L.precision_mode(), B, T)
-        assert wide % 100 in ((22, 21) if K > 1 else (14, 22)) and narrow != wide, (wide, narrow)
+        # (x6 multi-tap convs: the register-A tile 120, conv1d_x6ra.hip)
+        assert wide % 100 in ((22, 21, 20) if K > 1 else (14, 22)) and narrow != wide, (wide, narrow)
         st = torch.cuda.current_stream().cuda_stream
         outs = {}
         for cfg in (wide, narrow):
