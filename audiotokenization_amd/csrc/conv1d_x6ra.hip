@@ -242,8 +242,11 @@ static bool x6ra_b4_fits(const ConvArgs& a) {
 
 bool x6ra_applies(int K, int s, int d, int ps) {
   (void)d;
-  (void)ps;
-  return s == 1 && K > 1;  // multi-tap stride-1 convs and the phase launches with K / s >= 2 taps
+  // multi-tap stride-1 convs, the phase launches with K / s >= 2 taps, and the pointwise convs (K = 1: one K-step per
+  // chunk, the next chunk's planes stored mid-step, its successor's loads a step and a half ahead; measured slower than
+  // the 16-wave tile's pointwise path: C = 384 / 192 / 768 5.47 / 4.09 / 3.35 vs 4.63 / 3.45 / 3.03 ms with residual and
+  // dual output, profiles/r05j_ra_pointwise.txt -- the tables keep 122 there)
+  return s == 1 && (K > 1 || ps == 0);
 }
 
 const char* x6ra_kernel_name(bool b4) {

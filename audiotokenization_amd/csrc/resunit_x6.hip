@@ -528,13 +528,15 @@ static size_t ru_lds(const X6Tile& t, int C, int d, int P, int* bplane, int* hpl
 
 // k=7 taps per phase-1 K-step (h3), measured (profiles/r01g_ru_tps_prefetch_sweep.txt): 4 at C <= 64
 // (C = 48: -4 %), else 2 (C = 96: -2 %; 4 is 1.5x slower there), each only where the A buffers keep
-// the unit within the two-workgroups-per-CU LDS budget.  BC_RU_TPS forces 1 / 2 / 4 (timing experiments).
+// the unit within the two-workgroups-per-CU LDS budget.  x6 (round 5): 2 at C <= 64 -- the C = 48 unit 6.07 / 6.07 /
+// 6.14 -> 5.86 / 5.91 / 5.97 ms at d = 1 / 3 / 9 (profiles/r05i_ru48_tps2.txt); the same K order per output, so
+// bit-identical; C = 96 keeps 1 (two taps exceed the 80 KiB budget).  BC_RU_TPS forces 1 / 2 / 4 (timing experiments).
 static int ru_tps(const X6Tile& t, int C, int d, int P) {
   static const int forced = [] {
     const char* e = getenv("BC_RU_TPS");
     return e ? atoi(e) : 0;
   }();
-  if (P == 3) return 1;
+  if (P == 3 && (C > 64 || forced == 1 || forced == 4)) return 1;  // x6: two taps per K-step at C <= 64 (C = 48)
   if (forced == 1 || forced == 2 || forced == 4) return forced;
   int bp, hp;
   for (int tps : {4, 2})
@@ -604,8 +606,9 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
   }
   if (P != 3 && tps == 4)
     hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 4 : 1)>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
-  else if (P != 3 && tps == 2)
-    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 ? 2 : 1)>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
+  else if (tps == 2 && (P != 3 || (MT == 3 && NT == 1 && WM == 1)))  // (x6: the C = 48 tile only)
+    hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P, (P != 3 || (MT == 3 && NT == 1 && WM == 1) ? 2 : 1)>),
+                       dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
   else
     hipLaunchKernelGGL((resunit_x6_kernel<MT, NT, WM, WN, P>), dim3(a.nwg), dim3(NTHR), lds, st, a, e, r);
   BC_CHECK_LAUNCH();
