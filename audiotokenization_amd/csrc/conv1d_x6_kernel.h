@@ -389,6 +389,12 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       else store_b(v0, v1, Bs, xs);
     };
     auto step1 = [&](int c, auto& n0v, auto& n1v, auto& p0v, auto& p1v) {
+      // chunk c + 1's registers (loaded one step ago) are consumed HERE, before this step's A copy: the compiler
+      // does not count LDS-DMA copies, so its wait for them at the store below (or for the reuse of the other set
+      // by chunk c + 2's loads) drained vmcnt to zero -- the fresh copy and chunk c + 2's loads included, one
+      // full L2 + HBM round trip exposed per chunk.  Waited for here, they have had a whole step to land.
+#pragma unroll
+      for (int i = 0; i < (B4 ? IT4 : CI); ++i) asm volatile("" ::"v"(n0v[i]), "v"(n1v[i]));
       if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
       dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
       if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);

@@ -28,9 +28,10 @@ __device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, fl
 // (a power of two: exact) restores the fp32 dot product before the bias is added.
 // RP / rpre (MT == 1 only): the residual's 16-byte groups already loaded by the caller, one per n-tile,
 // for exactly the lanes / tiles that take the 16-byte path (conv_epilogue_res).
-// The 16-byte residual reads run one m-tile ahead of the m-tile being finished (two register sets):
-// issued next to the previous m-tile's arithmetic and stores instead of one dependent HBM round trip
-// per (m-tile, n-tile) (the pointwise convs' epilogue was a chain of MT x NT such round trips).
+// Loads run in passes of RPS m-tiles (all MT where the registers allow, else 2), each pass's per-row coefficients
+// and residual groups issued before its first store: vmcnt retires in issue order and counts stores, so a bias or
+// residual load issued behind m-tile i's stores can only be waited for once those stores have completed -- with a
+// load per m-tile that was one dependent store round trip per m-tile (6 per tile on the 192-row tiles, now 2).
 template <int MT, int NT, bool SC, bool RP>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
                                                    int col0, int lane, float xinv, const floatx4 (&rpre)[NT]) {
@@ -39,7 +40,17 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
   const bool snk = a.osa != nullptr;
   auto vec_tile = [&](int co, int nb) { return co < a.Cout && a.vec && nb + 3 < a.Nout; };
-  floatx4 rr[2][NT];
+  constexpr int RPS = (MT == 1 && RP) ? 1 : (MT * NT <= 8 ? MT : 2);
+  float pbias[RPS], psa[RPS], psb[RPS], psc[RPS];
+  auto load_p = [&](int i, int k) {
+    const int co = row0 + i * 16 + (lane & 15);
+    const bool ok = co < a.Cout;
+    pbias[k] = ok && a.bias ? a.bias[co] : 0.f;
+    psa[k] = ok && snk ? a.osa[co] : 0.f;
+    psb[k] = ok && snk ? a.osb[co] : 0.f;
+    psc[k] = SC && ok ? a.wsc[co] * xinv : 1.f;
+  };
+  floatx4 rr[RPS][NT];
   auto load_r = [&](int i, floatx4 (&d)[NT]) {
     const int co = row0 + i * 16 + (lane & 15);
 #pragma unroll
@@ -50,16 +61,22 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
         d[j] = *reinterpret_cast<const floatx4*>(rb + (long long)co * a.yT + a.ooff + nb);
     }
   };
-  if (!(MT == 1 && RP)) load_r(0, rr[0]);
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    if (!(MT == 1 && RP) && i + 1 < MT) load_r(i + 1, rr[(i + 1) & 1]);
+    if (i % RPS == 0) {  // the pass's coefficients and residual groups, before its first store
+#pragma unroll
+      for (int k = 0; k < RPS; ++k)
+        if (i + k < MT) {
+          load_p(i + k, k);
+          if (!(MT == 1 && RP)) load_r(i + k, rr[k]);
+        }
+    }
     const int co = row0 + i * 16 + (lane & 15);
     if (co >= a.Cout) continue;
-    const float bias = a.bias ? a.bias[co] : 0.f;
-    const float sa = snk ? a.osa[co] : 0.f;
-    const float sb = snk ? a.osb[co] : 0.f;
-    const float sc = SC ? a.wsc[co] * xinv : 1.f;
+    const float bias = pbias[i % RPS];
+    const float sa = psa[i % RPS];
+    const float sb = psb[i % RPS];
+    const float sc = psc[i % RPS];
     const long long rowoff = (long long)co * a.yT + a.ooff;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -68,7 +85,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
       if (vec_tile(co, nb)) {
         const long long yi = rowoff + nb;
         if (!BC_DOK(yi >= 0 && yi + 3 < a.ybs)) continue;  // debug build: the tile's 16 bytes inside the batch item
-        const floatx4 r = (MT == 1 && RP) ? rpre[j] : rr[i & 1][j];
+        const floatx4 r = (MT == 1 && RP) ? rpre[j] : rr[i % RPS][j];
         floatx4 v, sv;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
