@@ -14,8 +14,9 @@ import numpy as np
 
 # BIGCODEC_DEBUG=1: the bounds-checked debug build (build_lib.build(debug=True), _debug/; include/bigcodec.h
 # bc_debug_status) instead of the product library
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                       "_debug" if os.environ.get("BIGCODEC_DEBUG") == "1" else "")
+# BIGCODEC_LIB_DIR: another build's directory (A/B timing of two builds on one box; tools/lab5/)
+LIB_DIR = os.environ.get("BIGCODEC_LIB_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "_debug" if os.environ.get("BIGCODEC_DEBUG") == "1" else "")
 _LIB_PATH = os.path.join(LIB_DIR, "libbigcodec_hip.so")
 _lock = threading.Lock()
 _lib = None

@@ -606,7 +606,6 @@ int bc_dbg_fetch_conv1d_x6_p1(unsigned*);
 int bc_dbg_fetch_conv1d_x6_p2(unsigned*);
 int bc_dbg_fetch_conv1d_x6_p3(unsigned*);
 int bc_dbg_fetch_conv1d_x6ra(unsigned*);
-int bc_dbg_fetch_conv1d_x6pw(unsigned*);
 int bc_dbg_fetch_resunit_x6(unsigned*);
 int bc_dbg_fetch_resunit_rr(unsigned*);
 int bc_dbg_fetch_pw_presplit(unsigned*);
@@ -615,7 +614,7 @@ int bc_debug_status(unsigned* out) {
   if (!out) return BC_ERR_ARG;
   if (hipDeviceSynchronize() != hipSuccess) return BC_ERR_LAUNCH;
   out[0] = out[1] = 0;
-  int (*const fetch[])(unsigned*) = {bc_dbg_fetch_conv1d, bc_dbg_fetch_conv1d_x6_p1, bc_dbg_fetch_conv1d_x6_p2, bc_dbg_fetch_conv1d_x6ra, bc_dbg_fetch_conv1d_x6pw,
+  int (*const fetch[])(unsigned*) = {bc_dbg_fetch_conv1d, bc_dbg_fetch_conv1d_x6_p1, bc_dbg_fetch_conv1d_x6_p2, bc_dbg_fetch_conv1d_x6ra,
                                      bc_dbg_fetch_conv1d_x6_p3, bc_dbg_fetch_resunit_x6, bc_dbg_fetch_resunit_rr,
                                      bc_dbg_fetch_pw_presplit, bc_dbg_fetch_lstm_seq, bc_dbg_fetch_abi};
   for (auto f : fetch)

@@ -46,10 +46,6 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st);
 bool x6ra_applies(int K, int s, int d, int ps);
 const char* x6ra_kernel_name(bool b4);
 int x6ra_launch(ConvArgs& a, int B, hipStream_t st);
-// x6 pointwise convs on a 192 x 192 tile with double-buffered A and B (conv1d_x6pw.hip): routed from cfg 122, K = 1
-bool x6pw_fits(const ConvArgs& a);
-bool x6pw_on();
-int x6pw_launch(ConvArgs& a, int B, hipStream_t st);
 int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n);
 int conv_kernel_name(int cfg_id, int K, int s, int d, char* buf, int n);
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n);

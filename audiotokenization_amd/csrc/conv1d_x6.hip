@@ -434,8 +434,6 @@ int x6_kernel_name(int cfg, int K, int s, int d, char* buf, int n) {
   const int P = cfg_planes(cfg);
   if (P == 3 && cfg_base(cfg) == 120 && x6ra_applies(K, s, d, cfg_phase(cfg)))  // x6_launch's routing
     return snprintf(buf, n, "%s", x6ra_kernel_name(cfg_phase(cfg) == 0));
-  if (P == 3 && cfg_base(cfg) == 122 && cfg_phase(cfg) == 0 && K == 1 && s == 1 && x6pw_on())
-    return snprintf(buf, n, "conv1d_x6pw_kernel");  // (x6pw_fits at launch: every BigCodec k1 shape)
   const X6Variant v = x6_variant(t, P, K, s, d, cfg_phase(cfg));
   // (the 16-byte staging also needs Tin % 4 == 0 and 16-B aligned rows at launch, x6_b4_fits: true of every
   // BigCodec shape at the configs' clip lengths; a launch that fails it runs the single-float variant)
@@ -463,7 +461,6 @@ int x6_launch(ConvArgs& a, int B, int cfg, hipStream_t st) {
   }
   const int tile = cfg_base(cfg) % 100;
   if (cfg_planes(cfg) == 3 && tile == 20 && x6ra_applies(a.K, a.s, a.d, a.ps)) return x6ra_launch(a, B, st);
-  if (cfg_planes(cfg) == 3 && tile == 22 && x6pw_on() && x6pw_fits(a)) return x6pw_launch(a, B, st);
   switch (cfg_planes(cfg)) {
     case 1: return x6_launch_tile<1>(a, B, tile, st);
     case 2: return x6_launch_tile<2>(a, B, tile, st);

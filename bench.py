@@ -64,7 +64,7 @@ def kernel_peak(kname: str):
     """(peak in fp32-equivalent TFLOP/s, MFMA instructions per algorithmic FLOP pair, note)."""
     targs = [t.strip() for t in kname[kname.find("<") + 1:kname.rfind(">")].split(",")] if "<" in kname else []
     planes = targs[4] if kname.startswith(("conv1d_x6_kernel", "resunit_x6_kernel")) and len(targs) >= 5 else None
-    if kname.startswith(("conv1d_x6ra_kernel", "conv1d_x6pw_kernel")):  # x6 (three bf16 planes) only
+    if kname.startswith("conv1d_x6ra_kernel"):  # x6 (three bf16 planes) only
         planes = "3"
     if kname.startswith(("resunit_rr_kernel", "resunit_strip_kernel")):  # resunit_rr.hip: h3 (two fp16 planes) only
         planes = "2"
@@ -109,7 +109,7 @@ def roofline(summ, steps, probe):
     conv_ms = sum(v["ms_total"] for v in summ.values())
     traffic, mutil, tsrc = pmc_traffic(kname)
     peak, mult, note = kernel_peak(kname)
-    practical = probe / mult if kname.startswith(("conv1d_x6_kernel", "conv1d_x6ra_kernel", "conv1d_x6pw_kernel")) else None
+    practical = probe / mult if kname.startswith(("conv1d_x6_kernel", "conv1d_x6ra_kernel")) else None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "peak_note": note,
             "probe_bf16_tflops": round(probe, 1),

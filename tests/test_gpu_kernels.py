@@ -872,57 +872,6 @@ def test_b4_staging_bit_identical_to_single_float(dev, Cin, Cout, K, d, T, cfg):
         L._mode = old
 
 
-@pytest.mark.parametrize("Cin,Cout,B,T", [(192, 192, 2, 60000), (384, 384, 3, 2000), (768, 768, 2, 1004),
-                                          (384, 768, 1, 388), (1536, 768, 2, 196), (768, 1536, 1, 4)])
-def test_x6_pointwise_double_buffered(dev, Cin, Cout, B, T):
-    """x6 pointwise convs on the 1024-thread double-buffered 192 x 192 tile (conv1d_x6pw.hip: A and B both double
-    buffered, one barrier per 32-channel chunk) run when the input rows are 16-byte aligned; a 4-byte-offset copy of
-    the same input runs the 16-wave 192 x 256 tile.  Same K order per output, so y (residual added) and y2 (its Snake)
-    are bit-identical, ragged column tiles (T % 192 != 0) included, and y matches the fp64 oracle."""
-    old = L.precision_mode()
-    L.set_precision("x6")
-    try:
-        g = torch.Generator().manual_seed(Cin + 3 * Cout + T)
-        m = CV.WNConv1d(Cin, Cout, kernel_size=1)
-        conv = _rand_wn_conv(m, g)
-        x = torch.randn(B, Cin, T, generator=g)
-        res = torch.randn(B, Cout, T, generator=g)
-        ae = torch.rand(Cout, generator=g) + 0.5
-        ib = torch.rand(Cout, generator=g) + 0.5
-        sd = {k: v.detach() for k, v in conv.state_dict().items()}
-        m.to(dev)
-        st = torch.cuda.current_stream().cuda_stream
-        lib = L.load()
-        cfg = 122
-        name = ctypes.create_string_buffer(256)
-        assert lib.bc_conv1d_kernel_name(cfg, 1, 1, 1, name, 256) > 0
-        assert name.value.decode().startswith("conv1d_x6pw_kernel"), name.value
-        wp, bias = m.packed_as(cfg, dev)
-        buf = torch.empty(B * Cin * T + 4, device=dev)
-        rd, aed, ibd = res.to(dev), ae.to(dev), ib.to(dev)
-        outs = []
-        for off in (0, 1):
-            xd = buf[off:off + B * Cin * T].view(B, Cin, T)
-            xd.copy_(x.to(dev))
-            y = torch.full((B, Cout, T), float("nan"), device=dev)
-            y2 = torch.full((B, Cout, T), float("nan"), device=dev)
-            L.call("bc_conv1d_fwd", xd.data_ptr(), wp.data_ptr(), L.ptr(bias), rd.data_ptr(), aed.data_ptr(),
-                   ibd.data_ptr(), y.data_ptr(), y2.data_ptr(), B, Cin, T, Cout, T, 1, 1, 1, 0, 0, cfg, st)
-            torch.cuda.synchronize()
-            outs.append((y.cpu(), y2.cpu()))
-    finally:
-        L._mode = old
-    (ya, y2a), (yb, y2b) = outs
-    assert torch.equal(ya, yb), (ya - yb).abs().max()
-    assert torch.equal(y2a, y2b), (y2a - y2b).abs().max()
-    assert torch.isfinite(y2a).all()
-    sd64 = {k: v.double() for k, v in sd.items()}
-    tol = 3e-6 * max(1.0, np.sqrt(Cin / 64))
-    for s0 in sorted({0, max(0, T // 2 - 150), max(0, T - 300)}):
-        want = O.conv(x[..., s0:s0 + 300].double(), sd64, "", 1, 1, 0, 1, False) + res[..., s0:s0 + 300].double()
-        assert_close_rel(ya[..., s0:s0 + 300].double(), want, tol, f"x6pw window {s0}")
-
-
 @pytest.mark.parametrize("Cin,Cout,K,d,B,T", [(768, 768, 7, 1, 16, 25), (384, 384, 7, 3, 4, 125), (1024, 1536, 7, 1, 3, 5),
                                              (192, 192, 7, 9, 2, 60), (1536, 1536, 7, 1, 64, 24), (768, 768, 7, 9, 64, 120),
                                              (768, 768, 1, 1, 16, 25), (384, 384, 1, 1, 16, 125), (1536, 1536, 1, 1, 64, 24),
