@@ -478,8 +478,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
   }
 
   if (!BC_ABL(a.dbg, 8)) {
-    if constexpr (P == 2)
-      conv_epilogue<MT, NT, true>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
+    if constexpr (P == 2)  // (one m-tile per pass on the multi-tap paths: two spill there)
+      conv_epilogue<MT, NT, true, PW ? 0 : 1>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
     else
       conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
   }

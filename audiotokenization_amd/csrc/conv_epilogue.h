@@ -32,7 +32,10 @@ __device__ __forceinline__ float conv_epi_value(const ConvArgs& a, float acc, fl
 // and residual groups issued before its first store: vmcnt retires in issue order and counts stores, so a bias or
 // residual load issued behind m-tile i's stores can only be waited for once those stores have completed -- with a
 // load per m-tile that was one dependent store round trip per m-tile (6 per tile on the 192-row tiles, now 2).
-template <int MT, int NT, bool SC, bool RP>
+// RPSX: the pass size forced by the caller (0: the rule above; 1 where the two-m-tile passes' registers spill, e.g. the
+// h3 multi-tap 16-wave kernels: 7 -> 41 spilled VGPRs, the phase-decomposed strided launch 22 -> 31 ms per step,
+// profiles/r05r_ab_h3.txt)
+template <int MT, int NT, bool SC, bool RP, int RPSX = 0>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
                                                    int col0, int lane, float xinv, const floatx4 (&rpre)[NT]) {
   float* yb = a.y + (long long)b * a.ybs;
@@ -40,7 +43,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
   const float* rb = a.res ? a.res + (long long)b * a.rbs : nullptr;
   const bool snk = a.osa != nullptr;
   auto vec_tile = [&](int co, int nb) { return co < a.Cout && a.vec && nb + 3 < a.Nout; };
-  constexpr int RPS = (MT == 1 && RP) ? 1 : (MT * NT <= 8 ? MT : 2);
+  constexpr int RPS = (MT == 1 && RP) ? 1 : RPSX ? RPSX : (MT * NT <= 8 ? MT : 2);
   float pbias[RPS], psa[RPS], psb[RPS], psc[RPS];
   auto load_p = [&](int i, int k) {
     const int co = row0 + i * 16 + (lane & 15);
@@ -129,10 +132,10 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, const floa
   }
 }
 
-template <int MT, int NT, bool SC = false>
+template <int MT, int NT, bool SC = false, int RPSX = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const floatx4 (&acc)[MT][NT], int b, int row0,
                                               int col0, int lane, float xinv = 1.f) {
-  conv_epilogue_impl<MT, NT, SC, false>(a, acc, b, row0, col0, lane, xinv, acc[0]);
+  conv_epilogue_impl<MT, NT, SC, false, RPSX>(a, acc, b, row0, col0, lane, xinv, acc[0]);
 }
 template <int NT, bool SC = false>
 __device__ __forceinline__ void conv_epilogue_res(const ConvArgs& a, const floatx4 (&acc)[1][NT], int b, int row0,
