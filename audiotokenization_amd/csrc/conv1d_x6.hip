@@ -205,7 +205,9 @@ static int x6p3_preferred_cfg(int Cout, int Cin, int K, int s, int d) {
   const int Kp = (K + s - 1) / s;
   if (s == 2 && d == 1 && Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 2000 + 122;
   if (s >= 3 && s <= 16 && d == 1) {
-    if (Cout % 192 == 0 && Cout >= 1536 && fits(22, Kp, 1, 1)) return 1000 * s + (Kp > 1 ? ra2 : 122);
+    // (the register-A tile also beats the 256 x 256 one at 384 -> 768: 10.83 -> 10.39 ms, profiles/r05w_strided.txt)
+    if (Cout % 192 == 0 && (Cout >= 1536 || (ra2 == 120 && Kp > 1)) && fits(22, Kp, 1, 1))
+      return 1000 * s + (Kp > 1 ? ra2 : 122);
     if (Cout % 256 == 0 && fits(21, Kp, 1, 1)) return 1000 * s + 121;
     if (Cout % 192 == 0 && fits(22, Kp, 1, 1)) return 1000 * s + (Kp > 1 ? ra2 : 122);
   }
