@@ -22,12 +22,16 @@
 //                so one ds_read_b128 gives a lane its 8 k-values.  The next chunk's loads are issued
 //                at tap 0 and land while the current chunk's taps compute.
 #pragma once
+#include <type_traits>
+
 #include "bc_common.h"
 #include "bc_internal.h"
 #include "conv_epilogue.h"
 #include "x6_common.h"
 
 namespace bc {
+
+struct X6NoMid {};  // compute() without a mid-step hook
 
 // P = operand planes: 3 (x6, fp32-accurate), 2 ("h3": two fp16 planes, three products, fp32-class
 // accuracy at half the x6 MFMA count, x6_common.h) or 1 (plain bf16 products: the "bf16" precision
@@ -282,8 +286,10 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
 
   const int col_lane = (wn * NT * 16 + (lane & 15)) * a.s;
 
-  // one K32 unit: this wave's MT x NT tiles += A(buffer buf, slot tt) * B(tap-shifted columns)
-  auto compute = [&](int buf, int tt, int tap) {
+  // one K32 unit: this wave's MT x NT tiles += A(buffer buf, slot tt) * B(tap-shifted columns); mid() (unless
+  // X6NoMid) runs after m-tile 0's MFMAs
+  const X6NoMid nomid{};
+  auto compute = [&](int buf, int tt, int tap, auto&& mid) {
       const unsigned char* Ab = As + buf * (TPS * a_pieces * 1024) + tt * (a_pieces * 1024);
       // (n-tile j adds 16 * s columns: the swizzle of a stride-1 tile repeats every 8 columns)
       const unsigned char* Bcol = Br + bgrp(col_lane + tap * a.d, lane >> 4);
@@ -355,6 +361,13 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
             acc[i][j] = t;
           }
         }
+        if constexpr (!std::is_same<std::decay_t<decltype(mid)>, X6NoMid>::value) {
+          if (i == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            mid();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
       }
   };
 
@@ -398,7 +411,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
       dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
       if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);
-      compute(c & 1, 0, 0);
+      compute(c & 1, 0, 0, nomid);
       if (c + 1 < a.nchunks) {
         if constexpr (P == 2) mx(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
@@ -433,16 +446,32 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       if constexpr (DB) Br = Bs + (c & 1) * P * bplane;
       for (int tp = 0; tp < kst; ++tp) {
         const int step = c * kst + tp;
-        if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
-        if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) {
-          dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
-          stage_load(c + 1);
-        }
-        if (prio) __builtin_amdgcn_s_setprio(1);
+        if constexpr (B4 && TPS == 1) {
+          // the next step's copy and (step 0 of a chunk) the next chunk's loads, issued after this step's first
+          // m-tile of MFMAs: every wave leaves the barrier at once, and issuing the copies first held each SIMD's
+          // matrix pipe idle for their issue cost (one-tap B4 steps only: the single-float staging's registers
+          // spilled when live across the MFMAs)
+          auto mid = [&]() {
+            if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
+            if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) {
+              dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
+              stage_load(c + 1);
+            }
+          };
+          if (prio) __builtin_amdgcn_s_setprio(1);
+          compute(step & 1, 0, tp, mid);
+        } else {
+          if (step + 1 < nsteps && !BC_ABL(a.dbg, 1)) issue_a(step + 1, (step + 1) & 1);
+          if (tp == 0 && c + 1 < a.nchunks && !BC_ABL(a.dbg, 2)) {
+            dma_issue_order();  // the next chunk's loads stay behind the copy (the counted wait below)
+            stage_load(c + 1);
+          }
+          if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int tt = 0; tt < TPS; ++tt) {
-          const int tap = tp * TPS + tt;
-          if (TPS == 1 || tap < K) compute(step & 1, tt, tap);
+          for (int tt = 0; tt < TPS; ++tt) {
+            const int tap = tp * TPS + tt;
+            if (TPS == 1 || tap < K) compute(step & 1, tt, tap, nomid);
+          }
         }
         if (prio) __builtin_amdgcn_s_setprio(0);
         if constexpr (DB) {
