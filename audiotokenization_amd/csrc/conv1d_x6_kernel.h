@@ -408,10 +408,13 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       // full L2 + HBM round trip exposed per chunk.  Waited for here, they have had a whole step to land.
 #pragma unroll
       for (int i = 0; i < (B4 ? IT4 : CI); ++i) asm volatile("" ::"v"(n0v[i]), "v"(n1v[i]));
-      if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
-      dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
-      if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);
-      compute(c & 1, 0, 0, nomid);
+      // the next chunk's copy and chunk c + 2's loads go out after the first m-tile of MFMAs (as on the k7 path)
+      auto mid = [&]() {
+        if (c + 1 < a.nchunks && !BC_ABL(a.dbg, 1)) issue_a(c + 1, (c + 1) & 1);
+        dma_issue_order();  // chunk c + 2's loads stay behind the copy (the counted wait below)
+        if (c + 2 < a.nchunks && !BC_ABL(a.dbg, 2)) ld(c + 2, p0v, p1v);
+      };
+      compute(c & 1, 0, 0, mid);
       if (c + 1 < a.nchunks) {
         if constexpr (P == 2) mx(n0v, n1v, (c + 1) & 1);
         lds_barrier();  // every wave is done reading this chunk's B tile
