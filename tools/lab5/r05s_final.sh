@@ -3,7 +3,7 @@
 # x6 and h3 config-2 benches, smoke, every -m gpu test, the default bench line
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r05s
+O=gpurun_out/r05zc
 mkdir -p $O
 PMC_DIR=$O/pmc PMC_TIMEOUT=300 bash tools/gpu_pmc.sh || { echo "pmc failed $?"; exit 1; }
 echo pmc ok
