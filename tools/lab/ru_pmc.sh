@@ -12,7 +12,7 @@ i=0
 for ctr in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $R/p$i -o run -- \
-    python3 tools/ru_bench.py --precision h3 --iters 3 $ARGS > $R/p$i.log 2>&1
+    python3 tools/ru_bench.py --precision ${RU_PREC:-h3} --iters 3 $ARGS > $R/p$i.log 2>&1
   rc=$?; echo "[pass $i] exit $rc" >> $R/status.log
   [ $rc -ne 0 ] && exit $rc
 done
