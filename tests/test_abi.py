@@ -273,6 +273,17 @@ def test_kernel_names_come_from_the_launchers():
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 3), 3).endswith("false, 1, true, false>")
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(768, 384, 10, 5, 1, 3), 10, 5, 1) == \
         "conv1d_x6_kernel<6, 2, 2, 8, 2, false, 2, false, false>"
+    # x6 (the default): both stride-5 downsampling convs on the register-A tile (conv1d_x6ra.hip, round 5), the
+    # stride-2 ones and the k7 / pointwise convs on the 16-wave tile, the final k3 on the 256 x 256 tile
+    assert lib.bc_conv1d_select_cfg(768, 384, 10, 5, 1, 1) == 5120
+    assert lib.bc_conv1d_select_cfg(1536, 768, 10, 5, 1, 1) == 5120
+    assert L.conv_kernel_name(5120, 10, 5, 1) == "conv1d_x6ra_kernel<false>"
+    assert lib.bc_conv1d_select_cfg(384, 192, 4, 2, 1, 1) == 2122
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(384, 384, 7, 1, 9, 1), 7, 1, 9) == \
+        "conv1d_x6_kernel<6, 2, 2, 8, 3, false, 1, false, true>"
+    assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(384, 384, 1, 1, 1, 1), 1) == \
+        "conv1d_x6_kernel<6, 2, 2, 8, 3, true, 1, false, true>"
+    assert lib.bc_conv1d_select_cfg(1024, 1536, 3, 1, 1, 1) == 121
     # bf16 on the 16-wave tile: four taps per K-step over the double B buffer
     assert L.conv_kernel_name(lib.bc_conv1d_select_cfg(384, 384, 7, 1, 3, 2), 7, 1, 3) == \
         "conv1d_x6_kernel<6, 2, 2, 8, 1, false, 4, true, true>"
