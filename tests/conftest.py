@@ -71,3 +71,21 @@ def dev():
 
     _lib.load()  # the HIP library must load: no fallback
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _debug_build_bounds(request):
+    """Under the bounds-checked debug build (BIGCODEC_DEBUG=1: `BIGCODEC_DEBUG=1 pytest -m gpu` runs every GPU test on
+    it), a GPU test also fails when any kernel it launched counted a failed index check (include/bigcodec.h
+    bc_debug_status); the product build compiles no checks and this is a no-op."""
+    yield
+    if os.environ.get("BIGCODEC_DEBUG") != "1" or "gpu" not in request.keywords:
+        return
+    import torch
+
+    if not torch.cuda.is_available():
+        return
+    from audiotokenization_amd import _lib
+
+    st = _lib.debug_status()
+    assert st is None or st[0] == 0, f"debug build: {st[0]} failed index checks, first at source line {st[1]}"
