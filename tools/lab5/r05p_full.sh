@@ -3,7 +3,7 @@
 # rocprof kernel stats of the x6 bench
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r05p
+O=${FULL_OUT:-gpurun_out/r05p}
 mkdir -p $O
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke failed $?"; tail $O/smoke.txt; exit 1; }
 tail -1 $O/smoke.txt
