@@ -74,9 +74,11 @@ _SIGS = {
     "bc_resunit_kernel_name": (I, [I, I, I, C.c_char_p, I]),
     "bc_debug_status": (I, [P]),
     "bc_debug_selftest": (I, [I, P]),
+    "bc_launch_timer_enable": (I, [I]),
+    "bc_launch_timer_read": (I, [I, C.c_char_p, P, P, P]),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 16  # include/bigcodec.h BC_ABI_VERSION
+ABI_VERSION = 17  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
 
@@ -272,6 +274,26 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []  # (kernel symbol, flops, bytes, ev_start, ev_end)
+        self.lib_records = []  # (kernel symbol, ms, flops, bytes): launches made inside the library's composite calls
+
+    def drain_library(self):
+        """Collect the library's own launch-timer records (bc_launch_timer_read: the ResLSTM transposes, projection
+        and recurrence, the VQ), which the library brackets with HIP events on the launch stream."""
+        lib = load()
+        n = lib.bc_launch_timer_read(0, None, None, None, None)
+        if n < 0:
+            raise BigCodecLibraryError("bc_launch_timer_read failed")
+        if n == 0:
+            return
+        names = C.create_string_buffer(64 * n)
+        ms, fl, nb = (np.zeros(n, np.float32), np.zeros(n, np.float64), np.zeros(n, np.float64))
+        got = lib.bc_launch_timer_read(n, names, ms.ctypes.data, fl.ctypes.data, nb.ctypes.data)
+        if got < 0:
+            raise BigCodecLibraryError("bc_launch_timer_read failed")
+        raw = names.raw
+        for i in range(min(n, got)):
+            k = raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode()
+            self.lib_records.append((k, float(ms[i]), float(fl[i]), float(nb[i])))
 
     def begin(self):
         import torch
@@ -292,11 +314,13 @@ class KernelTimer:
         import torch
 
         torch.cuda.synchronize()
+        self.drain_library()
         out = {}
-        for k, fl, nb, e0, e1 in self.records:
+        rows = [(k, e0.elapsed_time(e1), fl, nb) for k, fl, nb, e0, e1 in self.records] + self.lib_records
+        for k, ms, fl, nb in rows:
             d = out.setdefault(k, dict(launches=0, ms_total=0.0, flops_total=0.0, bytes_total=0.0))
             d["launches"] += 1
-            d["ms_total"] += e0.elapsed_time(e1)
+            d["ms_total"] += ms
             d["flops_total"] += fl
             d["bytes_total"] += nb
         return out
@@ -306,8 +330,16 @@ _timer: KernelTimer | None = None
 
 
 def set_timer(t: KernelTimer | None) -> None:
+    """Start (t) / stop (None) timing: the Python-dispatched launches into t, and the library's launch timer
+    (bc_launch_timer_enable) for the launches inside its composite calls, drained into the timer that was active."""
     global _timer
-    _timer = t
+    prev, _timer = _timer, t
+    lib = load()
+    if prev is not None and prev is not t:
+        lib.bc_launch_timer_enable(0)
+        prev.drain_library()
+    if t is not None and prev is not t:
+        lib.bc_launch_timer_enable(1)
 
 
 def active_timer() -> KernelTimer | None:

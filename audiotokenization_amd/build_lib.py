@@ -24,7 +24,7 @@ OPS_LIB = os.path.join(PKG_DIR, "libbigcodec_ops.so")
 OPS_SRC = "torch_ops.cpp"
 ARCH = os.environ.get("BIGCODEC_ARCH", "gfx950")
 
-SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip", "conv1d_x6_p3.hip", "conv1d_x6ra.hip", "resunit_x6.hip", "resunit_rr.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip", "pw_presplit.hip",
+SOURCES = ["conv1d.hip", "conv1d_x6.hip", "conv1d_x6_p1.hip", "conv1d_x6_p2.hip", "conv1d_x6_p3.hip", "conv1d_x6ra.hip", "resunit_x6.hip", "resunit_w16.hip", "resunit_rr.hip", "elementwise.hip", "lstm.hip", "lstm_seq.hip", "pw_presplit.hip",
            "vq.hip", "resample.hip", "probe.hip", "abi.hip", "flac.cpp"]
 HEADERS = ["bc_common.h", "bc_internal.h", "conv_epilogue.h", "x6_common.h", "conv1d_x6_kernel.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",

@@ -3,11 +3,92 @@
 #include "bc_common.h"
 #include "bc_internal.h"
 
+#include <cstdio>
+#include <mutex>
+#include <string>
+#include <vector>
+
 using namespace bc;
+
+// ---- launch timer (bc_launch_timer_*): HIP events around the launches of the composite calls ----
+namespace bc {
+namespace {
+struct LTRec {
+  std::string name;
+  hipEvent_t e0, e1;
+  double flops, bytes;
+};
+std::mutex g_lt_mu;
+bool g_lt_on = false;
+std::vector<LTRec> g_lt;
+std::vector<hipEvent_t> g_lt_pool;
+hipEvent_t lt_event() {
+  if (!g_lt_pool.empty()) {
+    hipEvent_t e = g_lt_pool.back();
+    g_lt_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+}  // namespace
+
+LTScope::LTScope(const char* name, double flops, double bytes, hipStream_t st) : idx(-1) {
+  std::lock_guard<std::mutex> lk(g_lt_mu);
+  if (!g_lt_on) return;
+  hipEvent_t e0 = lt_event(), e1 = lt_event();
+  if (!e0 || !e1 || hipEventRecord(e0, st) != hipSuccess) return;
+  g_lt.push_back({name, e0, e1, flops, bytes});
+  idx = (int)g_lt.size() - 1;
+  st_ = st;
+}
+LTScope::~LTScope() {
+  if (idx < 0) return;
+  std::lock_guard<std::mutex> lk(g_lt_mu);
+  if (idx < (int)g_lt.size()) (void)hipEventRecord(g_lt[idx].e1, st_);
+}
+}  // namespace bc
+
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 extern "C" {
+
+static void lt_clear() {  // (caller holds g_lt_mu)
+  for (auto& r : bc::g_lt) {
+    bc::g_lt_pool.push_back(r.e0);
+    bc::g_lt_pool.push_back(r.e1);
+  }
+  bc::g_lt.clear();
+}
+
+int bc_launch_timer_enable(int on) {
+  std::lock_guard<std::mutex> lk(bc::g_lt_mu);
+  if (on && !bc::g_lt_on) lt_clear();  // a fresh recording
+  bc::g_lt_on = on != 0;
+  return BC_OK;
+}
+
+int bc_launch_timer_read(int max, char* names, float* ms, double* flops, double* bytes) {
+  std::lock_guard<std::mutex> lk(bc::g_lt_mu);
+  const int n = (int)bc::g_lt.size();
+  if (!names || !ms || !flops || !bytes || max <= 0) return n;  // the count only; nothing is cleared
+  int rc = n;
+  for (int i = 0; i < n; ++i) {
+    auto& r = bc::g_lt[i];
+    if (i < max) {
+      float t = 0.f;
+      if (hipEventSynchronize(r.e1) != hipSuccess || hipEventElapsedTime(&t, r.e0, r.e1) != hipSuccess) rc = -1;
+      snprintf(names + 64 * (long long)i, 64, "%s", r.name.c_str());
+      ms[i] = t;
+      flops[i] = r.flops;
+      bytes[i] = r.bytes;
+    }
+  }
+  lt_clear();
+  return rc;
+}
+
 
 int bc_abi_version(void) { return BC_ABI_VERSION; }
 
@@ -364,16 +445,27 @@ static int lstm_layer_dir(const float* lin, int Cin, const float* wih, const flo
   // (few columns, e.g. a streaming chunk: presplit_b walks every chunk of a 256-column tile in one workgroup, a fixed
   // ~220 us, so below 32 tiles the plain 322 launch, bit-identical, is faster; profiles/r04v_presplit_narrow.txt)
   const bool ps_size = tb >= 32 * 256 || g_lstm_presplit == 2;
-  if (psplit && g_lstm_presplit && cfg == 322 && ps_size && pw_presplit_ok(4 * H, Cin, tb))
-    rc = pw_presplit_launch(a, psplit, st);  // same planes, scales and MFMA chains as cfg 322: bit-identical
-  else if (psplit && g_lstm_presplit && cfg == 122 && ps_size && pw_presplit_x6_ok(4 * H, Cin, tb))
-    rc = pw_presplit_x6_launch(a, psplit, st);  // x6: the same planes and chains as cfg 122, 128-row tiles
-  else
-    rc = conv_launch(a, 1, cfg, st);
+  {  // (the launch timer: the pre-split launchers bracket their two kernels themselves)
+    const double pfl = 2.0 * 4 * H * (double)Cin * tb, pby = 4.0 * ((double)Cin + 4.0 * H) * tb;
+    if (psplit && g_lstm_presplit && cfg == 322 && ps_size && pw_presplit_ok(4 * H, Cin, tb)) {
+      rc = pw_presplit_launch(a, psplit, st);  // same planes, scales and MFMA chains as cfg 322: bit-identical
+    } else if (psplit && g_lstm_presplit && cfg == 122 && ps_size && pw_presplit_x6_ok(4 * H, Cin, tb)) {
+      rc = pw_presplit_x6_launch(a, psplit, st);  // x6: the same planes and chains as cfg 122, 128-row tiles
+    } else {
+      char nm[160];
+      if (conv_kernel_name(cfg, 1, 1, 1, nm, sizeof nm) < 0) snprintf(nm, sizeof nm, "conv cfg %d", cfg);
+      LTScope lt(nm, pfl, pby, st);
+      rc = conv_launch(a, 1, cfg, st);
+    }
+  }
   if (rc) return rc;
-  if (lstm_use_seq(H, mode))  // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
+  if (lstm_use_seq(H, mode)) {  // workspace tail (cst onwards) holds the persistent kernel's flags + h fragments
+    // algorithmic work: the recurrent GEMMs; bytes: gx read + the layer's output written
+    LTScope lt(lstm_seq_kernel_name(H, lstm_planes(mode), B < 64 ? B : 64), 2.0 * 4 * H * (double)H * tb,
+               4.0 * 5.0 * H * tb, st);
     return lstm_seq_launch(gx, reinterpret_cast<const unsigned short*>(whh), lout, cst, H, T, B, lstm_planes(mode), st,
                            h0, c0, hT, cT, call_status);
+  }
   if (h0 || c0 || hT || cT) return BC_ERR_UNSUPPORTED;  // carried state: the persistent kernel only
   const bool fast = lstm_fast_ok(H);
   for (int t = 0; t < T; ++t) {
@@ -406,7 +498,11 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
   float* yb = ya + tb * H;
   float* cst = yb + tb * H;
   float* const frag[2] = {cst + (long long)H * B, cst + (long long)H * B + lstm_frag_floats(B, H)};
-  int rc = btc_to_ctb_launch(x, xt, B, H, T, st);
+  int rc;
+  {
+    LTScope lt("btc_to_ctb_kernel", 0.0, 8.0 * H * tb, st);
+    rc = btc_to_ctb_launch(x, xt, B, H, T, st);
+  }
   if (rc) return rc;
   const float* lin = xt;
   float* lout = ya;
@@ -419,6 +515,7 @@ static int reslstm_impl(const float* x, float* out, int B, int H, int T, int num
     lin = lout;
     lout = (lout == ya) ? yb : ya;
   }
+  LTScope lt("ctb_to_btc_add_kernel", 0.0, 12.0 * H * tb, st);
   return ctb_to_btc_add_launch(lin, x, out_snake_alpha_exp, out_snake_inv_beta, out, B, H, T, st);
 }
 
@@ -494,6 +591,10 @@ int bc_vq_fwd(const float* z, const float* w_in, const float* b_in, const float*
     return BC_ERR_ARG;
   if (post_out && (!w_out || !b_out)) return BC_ERR_ARG;
   if (dim != 8) return BC_ERR_UNSUPPORTED;
+  // algorithmic work: in_proj + the n_codes distances + out_proj per frame; bytes: z read, post written, indices
+  const double fr = (double)B * T;
+  LTScope lt("vq_fwd_kernel", fr * 2.0 * (D * 8.0 + 8.0 * n_codes + (post_out ? 8.0 * D : 0.0)),
+             fr * (4.0 * D + (post_out ? 4.0 * D : 0.0) + 8.0 + (z_e_out ? 32.0 : 0.0)), S(stream));
   return vq_fwd_launch(z, w_in, b_in, codebook, codebook_norm, codebook_sq, w_out, b_out, idx,
                        z_e_out, post_out, B, D, T, n_codes, S(stream));
 }
@@ -607,6 +708,7 @@ int bc_dbg_fetch_conv1d_x6_p2(unsigned*);
 int bc_dbg_fetch_conv1d_x6_p3(unsigned*);
 int bc_dbg_fetch_conv1d_x6ra(unsigned*);
 int bc_dbg_fetch_resunit_x6(unsigned*);
+int bc_dbg_fetch_resunit_w16(unsigned*);
 int bc_dbg_fetch_resunit_rr(unsigned*);
 int bc_dbg_fetch_pw_presplit(unsigned*);
 int bc_dbg_fetch_lstm_seq(unsigned*);
@@ -615,7 +717,8 @@ int bc_debug_status(unsigned* out) {
   if (hipDeviceSynchronize() != hipSuccess) return BC_ERR_LAUNCH;
   out[0] = out[1] = 0;
   int (*const fetch[])(unsigned*) = {bc_dbg_fetch_conv1d, bc_dbg_fetch_conv1d_x6_p1, bc_dbg_fetch_conv1d_x6_p2, bc_dbg_fetch_conv1d_x6ra,
-                                     bc_dbg_fetch_conv1d_x6_p3, bc_dbg_fetch_resunit_x6, bc_dbg_fetch_resunit_rr,
+                                     bc_dbg_fetch_conv1d_x6_p3, bc_dbg_fetch_resunit_x6, bc_dbg_fetch_resunit_w16,
+                                     bc_dbg_fetch_resunit_rr,
                                      bc_dbg_fetch_pw_presplit, bc_dbg_fetch_lstm_seq, bc_dbg_fetch_abi};
   for (auto f : fetch)
     if (f(out)) return BC_ERR_LAUNCH;

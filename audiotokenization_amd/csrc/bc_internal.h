@@ -28,6 +28,9 @@ struct ConvArgs {
   int nchunks, win, bstage, astage;
   int bpitch;          // x6 kernel: bytes per B-tile column per plane (64: swizzled, stride 1; 80: strided)
   int prio;            // x6 kernel, 16-wave tile: s_setprio(1) for waves 8-15 for the whole launch (BC_X6_PRIO, A/B)
+  const float* isa;    // conv1d_x6_body<..., SIN>: Snake applied to the staged input, alpha_exp [Cin] / inv_beta [Cin]
+  const float* isb;
+  int sin_lds;         // SIN 2: byte offset of the [isa][isb] table in the kernel's dynamic LDS
   float inv_win;
   int ntm, ntn, nwg;
 };
@@ -68,8 +71,12 @@ int convT_interleave_launch(const float* ph, const float* ph2, float* y, float* 
 long long pw_presplit_bytes(int Cin, long long N);
 bool pw_presplit_ok(int Cout, int Cin, long long N);
 int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st);
-bool pw_presplit_x6_ok(int Cout, int Cin, long long N);  // the x6 variant (128 x 256 tile over cfg-322 weights)
+bool pw_presplit_x6_ok(int Cout, int Cin, long long N);  // the x6 variant (128 x 256 tile over cfg-122 weights)
 int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st);
+// one-launch ResidualUnit at C = 192 on the 16-wave 192 x 256 tile (resunit_w16.hip; x6, cfg 122)
+bool resunit_w16_ok(int C, int d, int P);
+int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s2a, const float* s2b, int B,
+                       hipStream_t st);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,
                    float* y, float* y2, int B, int C, int T, int d, int pl, int cfg, hipStream_t st,
@@ -115,6 +122,16 @@ int lstm_step_launch(const float* gx, const float* whh_p, float* y, float* cst, 
                      int T, int t, hipStream_t st);
 
 int mfma_probe_launch(float* out, int nwg, int iters, hipStream_t st);
+
+// Launch timer (bc_launch_timer_*, abi.hip): LTScope brackets the launches of its lifetime with HIP events on `st`
+// while the timer is enabled (a no-op otherwise).
+struct LTScope {
+  int idx;
+  hipStream_t st_ = nullptr;
+  LTScope(const char* name, double flops, double bytes, hipStream_t st);
+  ~LTScope();
+};
+const char* lstm_seq_kernel_name(int H, int planes, int nb);  // the variant lstm_seq_launch runs for nb clips
 
 int vq_prepare_launch(const float* cb, float* cbn, float* csq, int n, hipStream_t st);
 int vq_fwd_launch(const float* z, const float* w_in, const float* b_in, const float* cb,

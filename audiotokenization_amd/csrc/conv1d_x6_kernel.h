@@ -51,11 +51,20 @@ struct X6NoMid {};  // compute() without a mid-step hook
 // input chunk is read with 16-byte loads, each thread one channel pair x IT4 column quads (4 loads per thread on
 // the 16-wave tile instead of 12 single-float loads), staged into the same LDS image with the same block maxima:
 // outputs bit-identical to the single-float staging.
-template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false, bool B4 = false>
-// NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
-// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.  WM * WN = 16: one
-// 1024-thread workgroup (four waves per SIMD, <= 128 VGPRs).
-__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 4 : 2))) conv1d_x6_kernel(ConvArgs a) {
+//
+// The kernel body is conv1d_x6_body: the main loop over K, ending with the accumulators handed to `fin` (the
+// conv kernel's epilogue; resunit_w16.hip's bridge into the k=1 conv of a one-launch ResidualUnit).
+// SWAP (default): the input fragment is the MFMA's A operand, so the tile comes out transposed (a lane holds four
+// consecutive columns of one channel, conv_epilogue.h); !SWAP: weights as A, a lane holds four consecutive channels
+// of one column (the layout resunit_w16's bridge writes to LDS).  Same six products in the same order either way.
+// SIN: the input's Activation1d (Snake) applied to the staged chunk in registers before the split, so the producer
+// writes the raw tensor alone; per-channel coefficients from a.isa / a.isb (SIN 1) or from LDS at byte a.sin_lds,
+// [alpha_exp Cin][inv_beta Cin] (SIN 2, staged by the caller before the body's prologue barrier).
+extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
+
+template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS, bool DB, bool B4, bool SWAP, int SIN, class Fin>
+__device__ __forceinline__ void conv1d_x6_body(const ConvArgs& a, Fin&& fin) {
+  static_assert(!SIN || (!PW && P == 3), "snake on load: x6 multi-tap launches only");
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
@@ -67,7 +76,6 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
   // B4 iterations: ncol + 3 <= 4 * NQI * IT4 (pointwise: the input tile is the BN aligned columns)
   constexpr int IT4 = PW ? (BN / 4 + NQI - 1) / NQI : ((32 * X6_MAXCOL_ITERS + 6) / 4 + NQI - 1) / NQI;
   constexpr int NBL = B4 ? 2 * IT4 : 2 * CI;  // B load instructions per thread and chunk (the counted waits)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_x6[];
   __shared__ unsigned smax[2][NW];  // P == 2: per-wave maxima of the staged B chunk, by chunk parity
   typedef typename FragType<P>::type frag_t;
 
@@ -234,11 +242,35 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       *reinterpret_cast<unsigned*>(p + 2 * bplane) = l;
     }
   };
+
+  // SIN: the staged chunk's two channels (c0, c0 + 1 of this thread's pair) as one packed pair through the Snake
+  // (bit-identical to the producer epilogue's snake_pk on each; out-of-range loads read 0 and snake(0) = 0: the zero
+  // padding of the activated signal, as the reference pads it)
+  f32x2 sin_a = {0.f, 0.f}, sin_b = {0.f, 0.f};
+  auto sin_coefs = [&](int chunk) {
+    if constexpr (SIN == 1) {
+      const int c0 = chunk * X6_BKC + 2 * (B4 ? p4 : bp);
+      sin_a = (f32x2){c0 < a.Cin ? a.isa[c0] : 0.f, c0 + 1 < a.Cin ? a.isa[c0 + 1] : 0.f};
+      sin_b = (f32x2){c0 < a.Cin ? a.isb[c0] : 0.f, c0 + 1 < a.Cin ? a.isb[c0 + 1] : 0.f};
+    } else if constexpr (SIN == 2) {  // (Cin % 32 == 0: every pair is inside the table)
+      const int c0 = chunk * X6_BKC + 2 * (B4 ? p4 : bp);
+      const float* t = reinterpret_cast<const float*>(smem_x6 + a.sin_lds);
+      sin_a = *reinterpret_cast<const f32x2*>(t + c0);
+      sin_b = *reinterpret_cast<const f32x2*>(t + a.Cin + c0);
+    }
+  };
   auto store_b = [&](const float (&w0)[CI], const float (&w1)[CI], unsigned char* Bt, float sc) {
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
       const int col = bcol(i);
-      if (col < ncol) put(col, bp, w0[i], w1[i], Bt, sc);
+      if (col < ncol) {
+        if constexpr (SIN) {
+          const f32x2 v = snake_pk((f32x2){w0[i], w1[i]}, sin_a, sin_b);
+          put(col, bp, v.x, v.y, Bt, sc);
+        } else {
+          put(col, bp, w0[i], w1[i], Bt, sc);
+        }
+      }
     }
   };
   auto store_b4 = [&](const floatx4 (&w0)[B4 ? IT4 : 1], const floatx4 (&w1)[B4 ? IT4 : 1], unsigned char* Bt, float sc) {
@@ -247,7 +279,14 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
       const int col0 = 4 * (it * NQI + qb4) - r4;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (col0 + j >= 0 && col0 + j < ncol) put(col0 + j, p4, w0[it][j], w1[it][j], Bt, sc);
+        if (col0 + j >= 0 && col0 + j < ncol) {
+          if constexpr (SIN) {
+            const f32x2 v = snake_pk((f32x2){w0[it][j], w1[it][j]}, sin_a, sin_b);
+            put(col0 + j, p4, v.x, v.y, Bt, sc);
+          } else {
+            put(col0 + j, p4, w0[it][j], w1[it][j], Bt, sc);
+          }
+        }
     }
   };
   // the staging steps on whichever register set the variant uses
@@ -259,7 +298,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     if constexpr (B4) bmax_publish4(bq0, bq1, par);
     else bmax_publish(bv0, bv1, par);
   };
-  auto stage_store = [&](unsigned char* Bt, float sc) {
+  auto stage_store = [&](unsigned char* Bt, float sc, int chunk) {
+    if constexpr (SIN) sin_coefs(chunk);
     if constexpr (B4) store_b4(bq0, bq1, Bt, sc);
     else store_b(bv0, bv1, Bt, sc);
   };
@@ -352,12 +392,21 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
             // operands swapped (input as A): the tile comes out transposed, see conv_epilogue.h
             prefetch(j);
             floatx4 t = acc[i][j];
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
+            if constexpr (SWAP) {
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a2, t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a1, t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][P - 1], a0, t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a1, t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][1], a0, t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, t, 0, 0, 0);
+            } else {
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bf[j][0], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][1], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][P - 1], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[j][0], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][1], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], t, 0, 0, 0);
+            }
             acc[i][j] = t;
           }
         }
@@ -379,7 +428,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     lds_barrier();
     xs = bmax_scale(0);
   }
-  stage_store(Bs, xs);
+  stage_store(Bs, xs, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -486,14 +535,14 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
                 const float sn = bmax_scale((c + 1) & 1);
                 xn = sn < xs ? sn : xs;
               }
-              if (!BC_ABL(a.dbg, 4)) stage_store(Bs + ((c + 1) & 1) * P * bplane, xn);
+              if (!BC_ABL(a.dbg, 4)) stage_store(Bs + ((c + 1) & 1) * P * bplane, xn, c + 1);
             }
           }
         } else if (tp == kst - 1 && c + 1 < a.nchunks) {
           if constexpr (P == 2) stage_max((c + 1) & 1);
           lds_barrier();  // every wave is done reading this chunk's B tile
           if constexpr (P == 2) h3_next_scale((c + 1) & 1);
-          if (!BC_ABL(a.dbg, 4)) stage_store(Bs, xs);
+          if (!BC_ABL(a.dbg, 4)) stage_store(Bs, xs, c + 1);
         }
         // Only the next step's A copy (LDS-DMA, not tracked by the compiler) must have landed.  At
         // step 0 of a multi-step chunk the NBL B loads of the next chunk were issued after it and
@@ -509,12 +558,23 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 
     }
   }
 
-  if (!BC_ABL(a.dbg, 8)) {
-    if constexpr (P == 2)  // (one m-tile per pass on the multi-tap paths: two spill there)
-      conv_epilogue<MT, NT, true, PW ? 0 : 1>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
-    else
-      conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
-  }
+  fin(acc, b, m0, n0, wm, wn, lane, xs);
+}
+
+template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS = 1, bool DB = false, bool B4 = false>
+// NT == 1 tiles fit 128 VGPRs without spills: two 512-thread workgroups per CU where LDS allows, so
+// one workgroup's epilogue stores and operand loads overlap the other's MFMAs.  WM * WN = 16: one
+// 1024-thread workgroup (four waves per SIMD, <= 128 VGPRs).
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 16 ? 1 : (NT == 1 ? 4 : 2))) conv1d_x6_kernel(ConvArgs a) {
+  conv1d_x6_body<MT, NT, WM, WN, P, PW, TPS, DB, B4, true, 0>(
+      a, [&](floatx4 (&acc)[MT][NT], int b, int m0, int n0, int wm, int wn, int lane, float xs) {
+        if (!BC_ABL(a.dbg, 8)) {
+          if constexpr (P == 2)  // (one m-tile per pass on the multi-tap paths: two spill there)
+            conv_epilogue<MT, NT, true, PW ? 0 : 1>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane, 1.f / xs);
+          else
+            conv_epilogue<MT, NT>(a, acc, b, m0 + wm * MT * 16, n0 + wn * NT * 16, lane);
+        }
+      });
 }
 
 // ------------------------------------------------------------------------------------------------

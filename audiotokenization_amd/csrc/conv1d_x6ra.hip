@@ -15,7 +15,7 @@
 // Arithmetic: the same B planes (split2 of the same fp32 values), the same A planes (the cfg-120 / 122 packing: 12
 // m-tiles of 16 rows per 192-row group, identical for both tiles), the same chunk-major, tap-minor K order and the
 // same six-MFMA chain per output as conv1d_x6_kernel<..., P = 3>, and the shared epilogue: outputs are bit-identical
-// to the 16-wave tile (tests/test_gpu_kernels.py::test_x6ra_bit_identical).
+// to the 16-wave tile (tests/test_gpu_kernels.py::test_k7_tiles_large and test_h3_tiles_8_vs_16_waves, x6 cases).
 #include <type_traits>
 
 #include "bc_common.h"

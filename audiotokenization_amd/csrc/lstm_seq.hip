@@ -33,6 +33,8 @@
 //   Every poll is bounded: on timeout the kernel counts it in *status and all workgroups leave.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -824,6 +826,21 @@ int lstm_seq_launch(const float* gx, const unsigned short* whh, float* y, void* 
     BC_CHECK_LAUNCH();
   }
   return BC_OK;
+}
+
+// the symbol of the launch lstm_seq_launch makes for a launch of nb clips (its dispatch above; the launch timer)
+const char* lstm_seq_kernel_name(int H, int planes, int nb) {
+  static thread_local char buf[64];
+  const char* e = getenv("BC_LSTM_SEQ_HALVES");
+  const bool halves = !(e && atoi(e) == 1);
+  const char* e16 = getenv("BC_LSTM_NH16");
+  const bool h16 = !(e16 && atoi(e16) == 0) && nb <= 32;
+  const int ks = H / 128;
+  if (planes != 2 && !halves)
+    snprintf(buf, sizeof buf, "lstm_seq_x6_kernel<%d>", ks);
+  else
+    snprintf(buf, sizeof buf, "lstm_seq2_x6_kernel<%d, %d%s>", ks, planes, h16 ? ", 1" : "");
+  return buf;
 }
 
 }  // namespace bc

@@ -229,17 +229,17 @@ __global__ void __launch_bounds__(1024, 1) pw_presplit_kernel(ConvArgs a, const 
 // x6 (P = 3): the same idea without block scales (the 3 x bf16 split is exact per element).  Three planes of a
 // 256-column chunk are 48 KiB, so the 192-row GEMM's A + B double buffers (2 x 36 + 2 x 48 KiB) would exceed the
 // 160 KiB LDS: the x6 GEMM tile is 128 rows x 256 columns (16 waves of 64 x 32, 4 x 2 MFMA tiles each), A and B
-// double-buffered (2 x 24 + 2 x 48 = 144 KiB).  A comes from the weights packed for cfg 322 (192-row groups): its
+// double-buffered (2 x 24 + 2 x 48 = 144 KiB).  A comes from the weights packed for cfg 122 (192-row groups): its
 // 1-KiB pieces are per (16-row m-tile, plane, chunk), so any 16-row-aligned tile gathers them piece by piece.
 // Per output the same chunk order and the same six-MFMA chain as conv1d_x6_kernel<..., P = 3>: bit-identical to
-// the cfg-322 x6 launch (tests/test_gpu_kernels.py::test_lstm_projection_presplit_bit_identical[x6]).
+// the cfg-122 x6 launch (tests/test_gpu_kernels.py::test_lstm_projection_presplit_bit_identical[x6]).
 constexpr int PX_MT = 4, PX_NT = 2, PX_WM = 2, PX_WN = 8;
 constexpr int PX_BM = 16 * PX_MT * PX_WM;  // 128
 constexpr int PX_QA = PX_WM * PX_MT;       // 8 m-tiles
 constexpr int PX_APIECES = 3 * PX_QA;      // 24 pieces of a chunk's A block
 constexpr int PX_BPIECES = 3 * PS_PLANE / 1024;  // 48 pieces of a chunk's B block (3 per wave)
 constexpr int PX_LDS = 2 * 3 * PS_PLANE + 2 * PX_APIECES * 1024;  // 144 KiB
-constexpr int P322_QA = 12;                // m-tiles per 192-row group of the cfg-322 packing
+constexpr int P122_QA = 12;                // m-tiles per 192-row group of the cfg-122 packing
 
 __global__ void __launch_bounds__(256) presplit_b_x6_kernel(const float* __restrict__ x, unsigned char* __restrict__ planes,
                                                             int Cin, int N, int nch) {
@@ -306,14 +306,14 @@ __global__ void __launch_bounds__(1024, 1) pw_presplit_x6_kernel(ConvArgs a, con
 
   const unsigned char* wbase = reinterpret_cast<const unsigned char*>(a.w);
   const unsigned char* bblk = planes + (long long)nt_idx * nch * (3 * PS_PLANE);
-  // A piece q = plane * QA + local m-tile: m-tile g = m0 / 16 + local of the cfg-322 packing
+  // A piece q = plane * QA + local m-tile: m-tile g = m0 / 16 + local of the cfg-122 packing
   // [group g / 12][chunk][plane][g % 12][1 KiB]
   auto issue_a = [&](int c) {
     unsigned char* da = As + (c & 1) * (PX_APIECES * 1024);
     for (int q = wave; q < PX_APIECES; q += NW) {
       const int p = q / PX_QA, g = m0 / 16 + q % PX_QA;
       const unsigned char* src =
-          wbase + ((((long long)(g / P322_QA) * nch + c) * 3 + p) * P322_QA + g % P322_QA) * 1024;
+          wbase + ((((long long)(g / P122_QA) * nch + c) * 3 + p) * P122_QA + g % P122_QA) * 1024;
       __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (lds_void_t)(da + q * 1024), 16, 0, 0);
     }
   };
@@ -403,20 +403,23 @@ long long pw_presplit_bytes(int Cin, long long N) {
 }
 
 bool pw_presplit_x6_ok(int Cout, int Cin, long long N) {
-  return Cout % PX_BM == 0 && Cout % (16 * P322_QA) == 0 && Cin % X6_BKC == 0 && N > 0 && N <= 0x7fffffffLL &&
+  return Cout % PX_BM == 0 && Cout % (16 * P122_QA) == 0 && Cin % X6_BKC == 0 && N > 0 && N <= 0x7fffffffLL &&
          (long long)Cin * N * 4 <= 0x7fffffffffffLL;
 }
 
-// a: the pointwise conv as conv_launch would run it on cfg 322 in x6 (K = 1, stride 1, one batch item, x [Cin][N],
-// y [Cout][N]); w packed for cfg 322 (P = 3).  ws: pw_presplit_bytes(Cin, N) bytes (the three planes).
+// a: the pointwise conv as conv_launch would run it on cfg 122 in x6 (K = 1, stride 1, one batch item, x [Cin][N],
+// y [Cout][N]); w packed for cfg 122 (P = 3).  ws: pw_presplit_bytes(Cin, N) bytes (the three planes).
 int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st) {
   if (a.K != 1 || a.s != 1 || a.d != 1 || a.pl != 0 || a.ps || !ws) return BC_ERR_ARG;
   if (!pw_presplit_x6_ok(a.Cout, a.Cin, a.Nout) || a.Tin != a.Nout) return BC_ERR_UNSUPPORTED;
   const long long N = a.Nout;
   const int ntn = (int)((N + PS_BN - 1) / PS_BN), nch = a.Cin / X6_BKC;
   unsigned char* planes = reinterpret_cast<unsigned char*>(ws);
-  hipLaunchKernelGGL(presplit_b_x6_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, a.Cin, (int)N, nch);
-  BC_CHECK_LAUNCH();
+  {
+    LTScope lt("presplit_b_x6_kernel", 0.0, (4.0 + 6.0) * a.Cin * (double)N, st);  // fp32 in, three bf16 planes out
+    hipLaunchKernelGGL(presplit_b_x6_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, a.Cin, (int)N, nch);
+    BC_CHECK_LAUNCH();
+  }
   a.vec = conv_epilogue_vec_ok(a);
   a.ntm = a.Cout / PX_BM;
   a.ntn = ntn;
@@ -425,6 +428,7 @@ int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st) {
   if (nwg > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
   a.wsc = nullptr;
+  LTScope lt("pw_presplit_x6_kernel", 2.0 * a.Cout * (double)a.Cin * N, (6.0 * a.Cin + 4.0 * a.Cout) * (double)N, st);
   hipLaunchKernelGGL(pw_presplit_x6_kernel, dim3(a.nwg), dim3(1024), PX_LDS, st, a, planes);
   BC_CHECK_LAUNCH();
   return BC_OK;
@@ -444,8 +448,11 @@ int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st) {
   const int ntn = (int)((N + PS_BN - 1) / PS_BN), nch = a.Cin / X6_BKC;
   unsigned char* planes = reinterpret_cast<unsigned char*>(ws);
   float* scales = reinterpret_cast<float*>(planes + (long long)ntn * nch * 2 * PS_PLANE);
-  hipLaunchKernelGGL(presplit_b_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, scales, a.Cin, (int)N, nch);
-  BC_CHECK_LAUNCH();
+  {
+    LTScope lt("presplit_b_kernel", 0.0, (4.0 + 4.0) * a.Cin * (double)N, st);  // fp32 in, two fp16 planes out
+    hipLaunchKernelGGL(presplit_b_kernel, dim3(ntn), dim3(256), 0, st, a.x, planes, scales, a.Cin, (int)N, nch);
+    BC_CHECK_LAUNCH();
+  }
   a.vec = conv_epilogue_vec_ok(a);
   a.ntm = a.Cout / (16 * PS_MT * PS_WM);
   a.ntn = ntn;
@@ -455,6 +462,7 @@ int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st) {
   a.nwg = (int)nwg;
   a.wsc = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(a.w) +
                                          (long long)a.ntm * nch * PS_APIECES * 1024);  // 1 / row scales after the planes
+  LTScope lt("pw_presplit_kernel", 2.0 * a.Cout * (double)a.Cin * N, (4.0 * a.Cin + 4.0 * a.Cout) * (double)N, st);
   hipLaunchKernelGGL(pw_presplit_kernel, dim3(a.nwg), dim3(1024), PS_LDS, st, a, planes, scales);
   BC_CHECK_LAUNCH();
   return BC_OK;

@@ -500,11 +500,16 @@ __global__ void __launch_bounds__(RS_NTHR, 1) resunit_strip_kernel(RSArgs r, Con
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(r.x + (long long)b * r.xbs), 0, C * r.T * 4, 0x00020000);
     if (ws >= 0 && ws + W <= r.T) {  // interior window (uniform): no per-sample range checks
-      const int so = __builtin_amdgcn_readfirstlane(ws * 4);
+      // the window start rides in the 64-bit base of a second resource, not in the scalar offset: a buffer load whose
+      // soffset reaches 2^23 faults on gfx950 (found on conv1d_x6ra.hip), i.e. at ws > 2^21 samples here
+      const unsigned long long wb = (unsigned long long)(r.x + (long long)b * r.xbs + ws);
+      const unsigned wlo = __builtin_amdgcn_readfirstlane((unsigned)wb), whi = __builtin_amdgcn_readfirstlane((unsigned)(wb >> 32));
+      const __amdgpu_buffer_rsrc_t xw = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((unsigned long long)whi << 32) | wlo), 0, (C * r.T - ws) * 4, 0x00020000);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, nof + 128 * i, so, 0));
-        n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, nof + 128 * i + (unsigned)r.T * 4, so, 0));
+        n0[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xw, nof + 128 * i, 0, 0));
+        n1[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xw, nof + 128 * i + (unsigned)r.T * 4, 0, 0));
       }
     } else {
 #pragma unroll

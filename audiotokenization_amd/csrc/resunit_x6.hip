@@ -536,9 +536,13 @@ static int ru_tps(const X6Tile& t, int C, int d, int P) {
     const char* e = getenv("BC_RU_TPS");
     return e ? atoi(e) : 0;
   }();
-  if (P == 3 && (C > 64 || forced == 1 || forced == 4)) return 1;  // x6: two taps per K-step at C <= 64 (C = 48)
-  if (forced == 1 || forced == 2 || forced == 4) return forced;
   int bp, hp;
+  if (P == 3) {  // x6: two taps per K-step on the C = 48 tile (MT 3, NT 1, WM 1) only: launch_ru has no other x6 TPS-2
+                 // kernel, so any other tile's LDS size, launched template and kernel name are those of one tap
+    const bool t48 = t.MT == 3 && t.NT == 1 && t.WM == 1;
+    return t48 && C <= 64 && forced != 1 && forced != 4 && ru_lds(t, C, d, P, &bp, &hp, 2) <= ru_lds_budget(t) ? 2 : 1;
+  }
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
   for (int tps : {4, 2})
     if ((tps < 4 || C <= 64) && ru_lds(t, C, d, P, &bp, &hp, tps) <= ru_lds_budget(t)) return tps;
   return 1;
@@ -549,6 +553,8 @@ int resunit_select_cfg(int C, int d, int mode) {
   if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
+  // C = 192 (x6): the 16-wave 192 x 256 tile, k=1 weights streamed into registers (resunit_w16.hip)
+  if (!forced && resunit_w16_ok(C, d, P)) return 122;
   for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
@@ -618,6 +624,10 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
   if (mode < 1 || mode > 3 || !resunit_cfg_ok(cfg, C, d)) return -1;
+  if (cfg == 122) {  // resunit_w16.hip; the encoder flow activates on load unless BIGCODEC_RU_SNAKE_IN=0 (blocks.py)
+    const char* e = getenv("BIGCODEC_RU_SNAKE_IN");
+    return snprintf(buf, n, "resunit_w16_kernel<3, %d, true>", e && atoi(e) == 0 ? 0 : 2);
+  }
   if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
@@ -650,6 +660,12 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
   }();
   RUExtra r{w1, s2a, s2b, 0, 0, dbg, isa, isb};
   if (isa) a.x = x_raw;  // snake on load
+  if (cfg == 122) {
+    if (!resunit_w16_ok(C, d, 3)) return BC_ERR_UNSUPPORTED;
+    a.isa = isa;
+    a.isb = isb;
+    return resunit_w16_launch(a, e, w1, s2a, s2b, B, st);
+  }
 #define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
   case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \
   case 200 + ID: return launch_ru<MT, NT, WM, WN, 1>(a, e, r, B, st); \

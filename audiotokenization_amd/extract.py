@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import collections
 import os
+import weakref
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Tuple
 
@@ -241,7 +242,9 @@ class _SinkWriter:
         self.t.join()
 
 
-_CONTROL_GROUPS = {}  # (world group, ranks) -> the gloo control group of ShardedExtractor (one per process)
+# WORLD group -> {ranks: the gloo control group of ShardedExtractor} (one per process and world; weak keys, so a
+# destroyed world's groups are dropped with it)
+_CONTROL_GROUPS = weakref.WeakKeyDictionary()
 
 
 class ShardedExtractor:
@@ -300,10 +303,15 @@ class ShardedExtractor:
         if dist.get_backend(self.group) == "gloo":
             return self.group
         ranks = tuple(dist.get_process_group_ranks(self.group)) if self.group is not None else None
-        key = (id(dist.group.WORLD), ranks)
-        grp = _CONTROL_GROUPS.get(key)
+        # keyed on the WORLD group object itself (weakly: a destroyed world's entries go with it), not on id(): after
+        # destroy_process_group() and a re-init the new WORLD may reuse the freed object's address
+        world = dist.group.WORLD
+        per_world = _CONTROL_GROUPS.get(world)
+        if per_world is None:
+            per_world = _CONTROL_GROUPS[world] = {}
+        grp = per_world.get(ranks)
         if grp is None:
-            grp = _CONTROL_GROUPS[key] = dist.new_group(ranks=list(ranks) if ranks else None, backend="gloo")
+            grp = per_world[ranks] = dist.new_group(ranks=list(ranks) if ranks else None, backend="gloo")
         return grp
 
     def step(self, bi: int):

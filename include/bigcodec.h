@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BC_ABI_VERSION 16
+#define BC_ABI_VERSION 17
 
 int bc_abi_version(void);
 /* bc_build_digest: sha256 (64 hex characters) of the sources, headers and compiler flags this library was built
@@ -323,6 +323,19 @@ int bc_synth_clips(float* x, int B, long long T, long long clip0, void* stream);
  *   outside the debug words (the mechanism's own test).  Returns 3 in the product build. */
 int bc_debug_status(unsigned int* out);
 int bc_debug_selftest(int n, void* stream);
+
+/* ---- Launch timer of the composite calls (ABI 17; no reference counterpart: the measurement row SURVEY.md §8(d)) --
+ * The Python layer times every conv / ResidualUnit launch it makes itself; the kernels that bc_reslstm_fwd[_state],
+ * bc_reslstm_bidir_fwd and bc_vq_fwd launch inside one call (the layout transposes, the ResLSTM input projection and
+ * its pre-split planes, the persistent recurrence, the VQ) are only visible to the library.  While enabled, each of
+ * those launches is bracketed by HIP events recorded on the stream it is launched on.
+ * bc_launch_timer_enable(on): 1 starts a fresh recording (stale records are dropped), 0 stops it (records kept).
+ * bc_launch_timer_read(max, names, ms, flops, bytes): with max <= 0 or a null array, returns the number of records
+ *   and keeps them; otherwise synchronises the recorded events, copies the first max records (names: max x 64 bytes,
+ *   NUL-terminated kernel symbols; ms: event-timed duration; flops / bytes: the launch's algorithmic work), clears
+ *   all of them and returns their number (-1 on a HIP error). */
+int bc_launch_timer_enable(int on);
+int bc_launch_timer_read(int max, char* names, float* ms, double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

@@ -42,3 +42,23 @@ def test_committed_pmc_summaries_are_readable(tmp_path):
     assert bench.pmc_traffic(k, running="a" * 64, profiles=str(tmp_path)) == (100.0, 0.5, "r00_pmc_traffic.json")
     assert bench.pmc_traffic(k, running="b" * 64, profiles=str(tmp_path))[0] == 101.0
     assert bench.pmc_traffic(k, running="c" * 64, profiles=str(tmp_path)) == (None, None, None)
+
+
+def test_pmc_summary_takes_the_profiled_benchs_digest(tmp_path):
+    """tools/pmc_summary.py stamps a summary with the digest the profiled bench printed in its pass logs,
+    and with null when the passes disagree or a log has none -- never with the package's current library."""
+    import importlib.util
+    import json
+    import os
+
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(bench.REPO, "tools", "pmc_summary.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    d1, d2 = "a" * 64, "b" * 64
+    for p in ("FETCH_SIZE", "WRITE_SIZE", "MFMA"):
+        (tmp_path / f"{p}.log").write_text("rocprof noise\n" + json.dumps({"metric": "m", "lib_digest": d1}) + "\n")
+    assert ps.profiled_digest(str(tmp_path)) == d1
+    (tmp_path / "MFMA.log").write_text(json.dumps({"metric": "m", "lib_digest": d2}) + "\n")
+    assert ps.profiled_digest(str(tmp_path)) is None
+    (tmp_path / "MFMA.log").write_text("crashed before the line\n")
+    assert ps.profiled_digest(str(tmp_path)) is None

@@ -45,6 +45,7 @@ def _worker(rank, world, port, q):
 
 
 def _run(target, world, *extra):
+    # (8 ranks: the spawned interpreters import torch concurrently; the queue wait covers that)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -52,7 +53,7 @@ def _run(target, world, *extra):
     for p in procs:
         p.start()
     try:
-        results = dict(q.get(timeout=120) for _ in range(world))
+        results = dict(q.get(timeout=240) for _ in range(world))
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -88,7 +89,7 @@ def _fake_codes(ids):
     return ids[None, :, None] * 100 + torch.arange(NQ)[:, None, None] * 10 + torch.arange(NF)[None, None, :]
 
 
-def _extract_worker(rank, world, port, q, fail_rank, fail_batch):
+def _extract_worker(rank, world, port, q, fail_rank, fail_batch, n_clips=N_CLIPS):
     """extract_sharded itself (the product function) with a fake model that raises on one rank's batch."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -105,32 +106,38 @@ def _extract_worker(rank, world, port, q, fail_rank, fail_batch):
         return {"indices": _fake_codes(x[:, 0, 0].long())}
 
     sunk = {}
-    st = extract_sharded(model, N_CLIPS, 8, BATCH, rank=rank, world=world, device=torch.device("cpu"),
+    st = extract_sharded(model, n_clips, 8, BATCH, rank=rank, world=world, device=torch.device("cpu"),
                          sink=lambda cid, arr: sunk.__setitem__(cid, arr.copy()), source=_fake_source)
     q.put((rank, (st, sunk)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fail_rank,fail_batch", [(2, 1, 0), (3, 0, 0), (3, 2, 1)])
-def test_extract_sharded_survives_a_failed_batch(world, fail_rank, fail_batch):
+# (8, 5, 1, 37): the world config 4 names (8 ranks), 37 clips -> 4 or 5 per rank in batches of 3, so every rank's last
+# batch is short (1 or 2 clips) and rank 5's second -- its short last batch -- fails
+@pytest.mark.parametrize("world,fail_rank,fail_batch,n_clips", [(2, 1, 0, N_CLIPS), (3, 0, 0, N_CLIPS),
+                                                                (3, 2, 1, N_CLIPS), (8, 5, 1, 37), (8, 0, 0, 37)])
+def test_extract_sharded_survives_a_failed_batch(world, fail_rank, fail_batch, n_clips):
     """a rank whose batch raises must still join the batch's collectives, so the
     job finishes; the failure is counted (extract_indices.py:565-574) and every other clip arrives."""
     from audiotokenization_amd.extract import shard_range
 
-    results = _run(_extract_worker, world, fail_rank, fail_batch)
-    flo, fhi = shard_range(N_CLIPS, fail_rank, world)
+    results = _run(_extract_worker, world, fail_rank, fail_batch, n_clips)
+    flo, fhi = shard_range(n_clips, fail_rank, world)
     lost = list(range(flo + fail_batch * BATCH, min(flo + (fail_batch + 1) * BATCH, fhi)))
     assert lost, "the injected batch must hold real clips"
+    if world == 8:  # uneven shards and short last batches, as asked
+        sizes = [shard_range(n_clips, r, world)[1] - shard_range(n_clips, r, world)[0] for r in range(world)]
+        assert len(set(sizes)) == 2 and all(sz % BATCH for sz in sizes), sizes
     for r in range(world):
         st, sunk = results[r]
-        lo, hi = shard_range(N_CLIPS, r, world)
+        lo, hi = shard_range(n_clips, r, world)
         assert st.errors == (len(lost) if r == fail_rank else 0)
         assert st.error_items == (lost if r == fail_rank else [])
         assert st.clips == hi - lo - st.errors
-        assert st.job_errors == len(lost) and st.job_clips == N_CLIPS - len(lost)
+        assert st.job_errors == len(lost) and st.job_clips == n_clips - len(lost)
         if r == 0:
-            assert sorted(sunk) == [c for c in range(N_CLIPS) if c not in lost]
+            assert sorted(sunk) == [c for c in range(n_clips) if c not in lost]
             for cid, arr in sunk.items():
                 assert arr.dtype == np.int16 and arr.shape == (NF, NQ)
                 np.testing.assert_array_equal(arr, _fake_codes([cid])[:, 0, :].T.numpy())

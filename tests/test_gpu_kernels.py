@@ -488,6 +488,61 @@ def test_resunit_fused(dev, C, d, causal, B, T, ru_prec):
     assert torch.equal(lraw.cpu(), got) and torch.equal(lact.cpu(), act.cpu())
 
 
+@pytest.mark.parametrize("d,causal,B,T", [(1, False, 2, 1001), (3, False, 1, 24000), (9, False, 1, 24000),
+                                         (9, True, 2, 6000), (3, True, 1, 513), (1, False, 3, 256), (9, False, 2, 130),
+                                         (3, False, 2, 1001)])
+def test_resunit_w16_c192(dev, d, causal, B, T):
+    """The one-launch x6 ResidualUnit at C = 192 (resunit_w16.hip: the k7 main loop of the 16-wave tile, h through LDS,
+    k=1 weights streamed into registers) against the oracle, against the two-launch x6 path (k7 conv writing h, k=1
+    conv reading it: the same splits and the same per-output MFMA chains, so equal to fp32 rounding at most), with the
+    dual raw + next-Snake output, and snake on load (the producer writes only the raw tensor) bit-identical to a
+    producer-side Snake.  T = 1001 / 513 / 130 take the single-float staging (Tin % 4 != 0), the others the 16-byte one;
+    T = 130 / 256 / 513 leave partial 256-column tiles."""
+    from audiotokenization_amd.blocks import produce_conv
+
+    old = L.precision_mode()
+    L.set_precision("x6")
+    try:
+        g = torch.Generator().manual_seed(1920 + d * 7 + T)
+        ru = BL.ResidualUnit(192, dilation=d, causal=causal)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            ru.block[k].act.load_state_dict(_snake(192, g).state_dict())
+        nxt = M.Activation1d(activation=_snake(192, g))
+        x = torch.randn(B, 192, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        want = O.residual_unit(x, sd, "", d, causal, False)
+        want_s = O.snake_beta(want, nxt.act.alpha.detach(), nxt.act.beta.detach())
+        ru.to(dev)
+        nxt.to(dev)
+        cfg = ru._fused_cfg()
+        name = L.resunit_kernel_name(cfg, 192, d)
+        assert cfg == 122 and name.startswith("resunit_w16_kernel<3, "), (cfg, name)
+        xd = x.to(dev)
+        xa = ru.first_act(xd)
+        got = ru.flow(xd, xa)[0].cpu()
+        raw, act = ru.flow(xd, xa, want_raw=True, next_act=nxt)
+        _, act_only = ru.flow(xd, xa, want_raw=False, next_act=nxt)
+        assert ru.snake_on_load()
+        lazy = ru.flow(xd, None)[0].cpu()
+        lraw, lact = ru.flow(xd, None, want_raw=True, next_act=nxt)
+        _, h = produce_conv(ru.block[1], xa, None, want_raw=False, next_act=ru.block[2])
+        two = produce_conv(ru.block[3], h, residual=xd, want_raw=True, next_act=None)[0].cpu()
+    finally:
+        L._mode = old
+    diff = (got - two).abs().max().item()
+    print(f"w16 C=192 d={d} causal={causal} B={B} T={T}: fused vs two launches max |d| {diff:.3e}"
+          f" ({'bit-identical' if diff == 0 else 'not bit-identical'})")
+    assert_close_rel(got, want, 2e-5, f"w16 resunit d={d} T={T}")
+    assert_close_rel(got, two, 2e-6, f"w16 resunit d={d}: one launch vs two")
+    assert torch.equal(raw.cpu(), got)
+    assert_close_rel(act.cpu(), want_s, 5e-5, "w16 resunit + next snake")
+    assert torch.equal(act_only.cpu(), act.cpu())
+    assert torch.equal(lazy, got)
+    assert torch.equal(lraw.cpu(), got) and torch.equal(lact.cpu(), act.cpu())
+
+
 @pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, True, 1, 24000), (96, 3, False, 2, 513),
                                            (96, 9, False, 1, 4096), (64, 1, True, 2, 300), (16, 3, False, 3, 257)])
 def test_resunit_fused_bf16(dev, C, d, causal, B, T):
@@ -606,6 +661,40 @@ def test_resunit_c48_h3_sweep(dev, d, B, T):
     assert torch.equal(lazy, eager)
     assert torch.equal(lraw.cpu(), lazy)
     assert_close_rel(lact.cpu(), want_s, 5e-5, "resunit C=48 + next snake")
+
+
+@pytest.mark.parametrize("d", [1, 9])
+def test_resunit_strip_long_clip(dev, d):
+    """The h3 C = 48 strip kernel on ONE clip of T = 2 200 000 samples (92 s @24 kHz): window starts past 2^21 samples,
+    where the interior windows' byte offset (ws * 4) crosses 2^23 -- the scalar-offset range a gfx950 buffer load faulted
+    at; the offset now rides in the resource base.  Checked against the oracle in windows (the
+    unit is local: output [t0, t1) needs input [t0 - 3d, t1 + 3d)): before 2^21, across it, near 2^22 * 0.5 + T / 2, and
+    the clip's end (the real zero padding)."""
+    T = 2_200_000
+    old = L.precision_mode()
+    L.set_precision("h3")
+    try:
+        g = torch.Generator().manual_seed(4821 + d)
+        ru = BL.ResidualUnit(48, dilation=d)
+        _rand_wn_conv(ru.block[1], g)
+        _rand_wn_conv(ru.block[3], g)
+        for k in (0, 2):
+            ru.block[k].act.load_state_dict(_snake(48, g).state_dict())
+        x = torch.randn(1, 48, T, generator=g)
+        sd = {k: v.detach() for k, v in ru.state_dict().items()}
+        ru.to(dev)
+        name = L.resunit_kernel_name(ru._fused_cfg(), 48, d)
+        assert name == f"resunit_strip_kernel<{d}>", name
+        got = ru.flow(x.to(dev), None)[0].cpu()
+        torch.cuda.synchronize()
+    finally:
+        L._mode = old
+    h = 3 * d
+    for t0 in (1000, 2_097_000, 2_150_000, T - 3000):
+        t1 = min(t0 + 3000, T)
+        lo, hi = max(t0 - h, 0), min(t1 + h, T)
+        want = O.residual_unit(x[..., lo:hi], sd, "", d, False, False)[..., t0 - lo:t0 - lo + (t1 - t0)]
+        assert_close_rel(got[..., t0:t1], want, 2e-5, f"strip d={d} T={T} window {t0}")
 
 
 @pytest.mark.parametrize("Cin,Cout,K,s,d", [(384, 384, 7, 1, 9), (48, 96, 4, 2, 1), (768, 768, 1, 1, 1)])

@@ -94,7 +94,8 @@ def test_bf16_precision_index_mismatch_rate(dev, golden):
         L._mode = old
     rate = float((codes != g["codes"]).mean())
     print(f"bf16 conv products: index mismatch rate {rate:.4f} over {codes.size} frames")
-    assert rate < 0.25
+    # measured 0.042 (5 of 120 frames; 2.9 % over config 5's 115 200): the bound is about twice the config-5 rate
+    assert rate < 0.06
 
 
 def test_lightning_shim_surface(dev, golden):

@@ -39,6 +39,30 @@ def mean(v):
     return sum(v) / len(v) if v else 0.0
 
 
+def profiled_digest(src):
+    """The library digest the profiled bench itself printed (its JSON line's lib_digest) in every pass log of
+    tools/gpu_pmc.sh, or None when a log lacks it or the passes ran different libraries (reading the
+    package's .so here would stamp an A/B build's or a rebuilt library's counters with the wrong digest)."""
+    digs = set()
+    for pass_ in ("FETCH_SIZE", "WRITE_SIZE", "MFMA"):
+        path = os.path.join(src, pass_ + ".log")
+        if not os.path.exists(path):
+            continue
+        dig = None
+        for line in open(path, errors="replace"):
+            line = line.strip()
+            if line.startswith("{") and '"lib_digest"' in line:
+                try:
+                    dig = json.loads(line).get("lib_digest")
+                except ValueError:
+                    pass
+        digs.add(dig)
+    if len(digs) != 1 or None in digs:
+        print(f"pmc_summary: pass logs name digests {sorted(map(str, digs))}: lib_digest left null", file=sys.stderr)
+        return None
+    return digs.pop()
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     fetch = load(os.path.join(src, "FETCH_SIZE", "run_counter_collection.csv"))
@@ -57,10 +81,7 @@ def main():
             d["mfma_util"] = mean(util)
             d["mfma_busy_cycles"] = mean(busy[k])
         res[k] = d
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from audiotokenization_amd import build_lib
-
-    out = {"lib_digest": build_lib.lib_digest(build_lib.LIB),  # bench.py reports this traffic only on that library
+    out = {"lib_digest": profiled_digest(src),  # bench.py reports this traffic only on that library
            "note": "per-launch averages; traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 wide-read correction); "
                    "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
            "kernels": res}
