@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
       const int k = q / 3, part = q % 3;
       const float* src = k == 0 ? a.bias : k == 1 ? r.s2a : k == 2 ? r.s2b : k == 3 ? e.bias : k == 4 ? e.osa
                          : k == 5 ? e.osb : k == 6 ? a.isa : a.isb;
-      unsigned char* dst = smem_x6 + W16_COEF + k * (W16_C * 4) + part * 256;
+      unsigned char* dst = smem_xb + W16_COEF + k * (W16_C * 4) + part * 256;
       if (src)
         __builtin_amdgcn_global_load_lds((const void*)(src + part * 64 + lane), (lds_void_t)dst, 4, 0, 0);
       else
@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
   conv1d_x6_body<6, 2, 2, 8, P, false, 1, false, B4, false, SIN>(
       a, [&](floatx4 (&acc)[6][2], int b, int m0, int n0, int wm, int wn, int lane, float) {
         (void)m0;
-        unsigned char* Hs = smem_x6;  // aliases the phase-1 B tile and A buffers: every wave has passed the last
+        unsigned char* Hs = smem_xb;  // aliases the phase-1 B tile and A buffers: every wave has passed the last
                                       // K-step's barrier and no copy is in flight (the last step issued none)
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int mg = wave & 3, ng = wave >> 2;  // phase 2: rows 48 mg .. + 48, local n-tiles 2 ng, 2 ng + 1
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
 #pragma unroll
           for (int i = 0; i < 6; ++i) {
             const int co = wm * 96 + i * 16 + (lane >> 4) * 4;  // 4 consecutive channels co..co+3
-            const float* cf = reinterpret_cast<const float*>(smem_x6 + W16_COEF) + co;
+            const float* cf = reinterpret_cast<const float*>(smem_xb + W16_COEF) + co;
             const floatx4 bias = *reinterpret_cast<const floatx4*>(cf);
             const floatx4 sa = *reinterpret_cast<const floatx4*>(cf + W16_C);
             const floatx4 sb = *reinterpret_cast<const floatx4*>(cf + 2 * W16_C);
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
             if (acc2[0][0][0] == 1234.5f && rr[0][0][0] == 1.f) e.y[0] = 0.f;  // keep the work alive
             return;
           }
-          const float* cf = reinterpret_cast<const float*>(smem_x6 + W16_COEF);
+          const float* cf = reinterpret_cast<const float*>(smem_xb + W16_COEF);
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
             const int co = mg * 48 + i * 16 + (lane & 15);

@@ -1,7 +1,6 @@
 #!/bin/bash
 # round 6: the whole GPU suite on the tree with the C = 192 one-launch unit, the strip-kernel offset fix and the
-# library launch timer; smoke; the x6 bench line (kernels_top now with the ResLSTM / VQ launches); the x6 C = 48 / 96
-# unit ablation on the BIGCODEC_ABLATION build (BC_RU_DEBUG bits)
+# library launch timer; smoke; the x6 bench line (kernels_top now with the ResLSTM / VQ launches)
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/r06c
@@ -16,11 +15,4 @@ import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
 print('bench', d['value'], d['ms_per_step'], r['probe_bf16_tflops'], d['parity']['vs_reference_fixture']['index_mismatches'], 'h3', d['h3']['value'])
 print('timed total', r['all_timed_kernels_ms_per_step'], 'conv', r['all_python_conv_kernels_ms_per_step'])
 for k in r['kernels_top']: print('   ', k['kernel'][:60], k['bound'], k['launches_per_step'], k['ms_per_step'], k['frac_mfma_spec'], k['frac_hbm'])"
-for C in 48 96; do
-  T=$((240000 * 48 / C))
-  for dbg in 0 1 2 4 8 16 32 64 0; do
-    BIGCODEC_PKG_ROOT=$PWD/gpurun_abl BC_RU_DEBUG=$dbg timeout -k 10 100 python tools/ru_bench.py --C $C --d 3 --T $T --precision x6 --lazy --iters 10 > $O/t.txt 2>&1 || { echo "ru failed"; tail $O/t.txt; exit 1; }
-    echo "C=$C dbg $dbg: $(grep resunit $O/t.txt)" | tee -a $O/ru_abl.txt
-  done
-done
 echo done
