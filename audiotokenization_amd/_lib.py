@@ -78,6 +78,9 @@ _SIGS = {
     "bc_launch_timer_read": (I, [I, C.c_char_p, P, P, P]),
 }
 EXPORTED = tuple(_SIGS)
+# measurement-only entry points a library of an earlier ABI lacks (tools/lab* A/B runs load such builds through
+# BIGCODEC_LIB_DIR); the product's own library exports them all (test_abi)
+_OPTIONAL = ("bc_launch_timer_enable", "bc_launch_timer_read")
 ABI_VERSION = 17  # include/bigcodec.h BC_ABI_VERSION
 
 _ERR = {1: "bad argument", 2: "HIP launch error", 3: "unsupported shape"}
@@ -107,6 +110,8 @@ def load(path: str | None = None):
         except OSError as e:  # pragma: no cover - depends on the machine
             raise BigCodecLibraryError(f"failed to load {p}: {e}") from e
         for name, (res, args) in _SIGS.items():
+            if name in _OPTIONAL and not hasattr(lib, name):
+                continue  # an older build loaded for an A/B timing (BIGCODEC_LIB_DIR): timing hooks only
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -280,6 +285,8 @@ class KernelTimer:
         """Collect the library's own launch-timer records (bc_launch_timer_read: the ResLSTM transposes, projection
         and recurrence, the VQ), which the library brackets with HIP events on the launch stream."""
         lib = load()
+        if not hasattr(lib, "bc_launch_timer_read"):
+            return
         n = lib.bc_launch_timer_read(0, None, None, None, None)
         if n < 0:
             raise BigCodecLibraryError("bc_launch_timer_read failed")
@@ -335,6 +342,8 @@ def set_timer(t: KernelTimer | None) -> None:
     global _timer
     prev, _timer = _timer, t
     lib = load()
+    if not hasattr(lib, "bc_launch_timer_enable"):
+        return
     if prev is not None and prev is not t:
         lib.bc_launch_timer_enable(0)
         prev.drain_library()
