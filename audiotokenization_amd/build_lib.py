@@ -31,6 +31,8 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={A
           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
 if os.environ.get("BIGCODEC_ABLATION") == "1":  # tools/*_ablation.sh only: compiles the work-skipping switches in
     CFLAGS.append("-DBC_ABLATION")
+if os.environ.get("BIGCODEC_NO_XCD_REMAP") == "1":  # experiment builds only: workgroups in the dispatcher's order
+    CFLAGS.append("-DBC_NO_XCD_REMAP")
 
 
 def _hipcc() -> str:

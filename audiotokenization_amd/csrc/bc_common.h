@@ -132,6 +132,9 @@ __device__ __forceinline__ f32x2 snake_pk(f32x2 x, f32x2 alpha_exp, f32x2 inv_be
 // bijective"): workgroups that the dispatcher deals to the same XCD (ids b, b+8, b+16, ...) receive
 // consecutive logical ids, so neighbouring tiles that share an input panel share one L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+#ifdef BC_NO_XCD_REMAP  // experiment builds only (BIGCODEC_NO_XCD_REMAP=1): the dispatcher's own order
+  return orig;
+#endif
   const int q = nwg / 8, r = nwg % 8;
   const int xcd = orig % 8, loc = orig / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;

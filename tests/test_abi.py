@@ -296,6 +296,14 @@ def test_kernel_names_come_from_the_launchers():
     for C, d in ((48, 1), (96, 3)):
         nb = L.resunit_kernel_name(lib.bc_resunit_select_cfg(C, d, 2), C, d)
         assert nb.startswith("resunit_x6_kernel<") and re.search(r", 1, [124]>$", nb), nb
+    # x6: the C = 48 unit at two taps per K-step, C = 96 at one, C = 192 the 16-wave unit; the x6 C = 32 / 16 tiles
+    # launch one tap per K-step, and their names say so
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 3, 1), 48, 3) == "resunit_x6_kernel<3, 1, 1, 8, 3, 2>"
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 1), 96, 3) == "resunit_x6_kernel<6, 1, 1, 8, 3, 1>"
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(192, 3, 1), 192, 3).startswith("resunit_w16_kernel<3, ")
+    for C in (16, 32):
+        nx = L.resunit_kernel_name(lib.bc_resunit_select_cfg(C, 3, 1), C, 3)
+        assert re.search(r", 3, 1>$", nx), nx
     with pytest.raises(L.BigCodecLibraryError):
         L.conv_kernel_name(12345, 7)
 

@@ -13,6 +13,12 @@ def test_kernel_peak_by_operand_planes():
         "resunit_x6_kernel<6, 1, 1, 8, 1, 2>": bf16,
         "resunit_rr_kernel<96, 2, 1>": h3,
         "resunit_strip_kernel<3>": h3,
+        "resunit_x6_kernel<3, 1, 1, 8, 3, 2>": x6,
+        "resunit_w16_kernel<3, 2, true>": x6,
+        "lstm_seq2_x6_kernel<12, 3>": x6,
+        "lstm_seq2_x6_kernel<12, 2, 1>": h3,
+        "pw_presplit_x6_kernel": x6,
+        "pw_presplit_kernel": h3,
         "conv1d_mfma_kernel<3, 1, 4, 4, 4>": bench.FP32_MFMA_PEAK_TFLOPS,
     }
     for name, peak in cases.items():
