@@ -839,7 +839,8 @@ const char* lstm_seq_kernel_name(int H, int planes, int nb) {
   if (planes != 2 && !halves)
     snprintf(buf, sizeof buf, "lstm_seq_x6_kernel<%d>", ks);
   else
-    snprintf(buf, sizeof buf, "lstm_seq2_x6_kernel<%d, %d%s>", ks, planes, h16 ? ", 1" : "");
+    snprintf(buf, sizeof buf, "lstm_seq2_x6_kernel<%d, %d, %d>", ks, planes, h16 ? 1 : 2);  // (NTH spelled out, as
+                                                                                               // rocprofv3 names it)
   return buf;
 }
 

@@ -95,6 +95,7 @@ def test_conv1d(dev, case, prec):
     (192, 192, 7, 1, 9, 700, (320, 322)), (384, 384, 7, 1, 3, 515, (320, 322)), (192, 192, 7, 1, 1, 256, (320, 322)),
     (768, 768, 7, 1, 9, 300, (320, 322)), (384, 768, 10, 5, 1, 300, (5320, 5322)),
     (192, 384, 4, 2, 1, 520, (2320, 2322)), (96, 192, 4, 2, 1, 600, (2320, 2322)),
+    (96, 192, 4, 2, 1, 2001, (2320, 2322)), (192, 384, 4, 2, 1, 1542, (2320, 2322)),
     (768, 1536, 10, 5, 1, 130, (5320, 5322))])
 @pytest.mark.parametrize("tprec", ["h3", "bf16", "x6"])
 def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
@@ -103,7 +104,9 @@ def test_h3_tiles_8_vs_16_waves(dev, Cin, Cout, K, s, d, T, cfgs, tprec):
     and runs the same per-output MFMA chains: bit-identical outputs, and within the conv tolerance of the
     oracle.  The bf16 planes (cfg - 100) and the x6 planes (cfg - 200: three bf16 planes, the 16-wave tile
     without the A-fragment prefetch) run the same two tiles; in x6 the 8-wave tile (120) is the register-A kernel
-    (conv1d_x6ra.hip), bit-identical to the 16-wave one."""
+    (conv1d_x6ra.hip), bit-identical to the 16-wave one.  Stride 2 also at T = 2001 / 1542 (interior column tiles,
+    the odd padding, Tin % 4 != 0: the round-6 16-byte quad staging was checked against these and measured without
+    gain, profiles/r06i_stride2_quad_staging_rejected.txt)."""
     old = L.precision_mode()
     L.set_precision(tprec)
     if tprec != "h3":
