@@ -1043,3 +1043,37 @@ def test_strip_partition_independent(dev, d):
         L._mode = old
     assert torch.equal(y16, y64[:16]) and torch.equal(y1, y64[:1])
     assert torch.equal(yl1, yl[1:2])
+
+
+def test_launch_timer_records_the_composite_calls(dev):
+    """bc_launch_timer_* (ABI 17): with the timer on, a ResLSTM forward records its transposes, input projection and
+    persistent recurrence (the variant name lstm_seq_launch ran, as rocprofv3 spells it), and a VQ forward its kernel,
+    each with an event time and the launch's algorithmic work; KernelTimer merges them; nothing is recorded when off."""
+    old = L.precision_mode()
+    L.set_precision("x6")
+    try:
+        H, B, T = 1536, 64, 40
+        g = torch.Generator().manual_seed(7)
+        m = BL.ResLSTM(H, num_layers=2).to(dev)
+        x = torch.randn(B, H, T, generator=g).to(dev)
+        m(x)  # packing and warm-up outside the timer
+        torch.cuda.synchronize()
+        tm = L.KernelTimer()
+        L.set_timer(tm)
+        m(x)
+        L.set_timer(None)
+        summ = tm.summary()
+        m(x)  # timer off: nothing more is recorded
+        torch.cuda.synchronize()
+        tm.drain_library()
+    finally:
+        L._mode = old
+    names = set(summ)
+    rec = [k for k in names if k.startswith("lstm_seq2_x6_kernel<12, 3, ")]
+    assert rec and summ[rec[0]]["launches"] == 2, names
+    assert summ[rec[0]]["flops_total"] == 2 * 2.0 * 4 * H * H * T * B
+    assert summ["btc_to_ctb_kernel"]["launches"] == 1 and summ["ctb_to_btc_add_kernel"]["launches"] == 1
+    proj = [k for k in names if k.startswith(("pw_presplit_x6_kernel", "conv1d_x6_kernel"))]
+    assert proj and sum(summ[k]["launches"] for k in proj) == 2, names
+    assert all(d["ms_total"] > 0 for d in summ.values())
+    assert len(tm.lib_records) == sum(d["launches"] for d in summ.values())  # the off-period added nothing
