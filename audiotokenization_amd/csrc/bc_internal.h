@@ -73,9 +73,9 @@ bool pw_presplit_ok(int Cout, int Cin, long long N);
 int pw_presplit_launch(ConvArgs& a, void* ws, hipStream_t st);
 bool pw_presplit_x6_ok(int Cout, int Cin, long long N);  // the x6 variant (128 x 256 tile over cfg-122 weights)
 int pw_presplit_x6_launch(ConvArgs& a, void* ws, hipStream_t st);
-// one-launch ResidualUnit at C = 192 on the 16-wave 192 x 256 tile (resunit_w16.hip; x6, cfg 122)
+// one-launch ResidualUnit at C = 192 on the 16-wave 192 x 256 tile (resunit_w16.hip; x6 cfg 122, bf16 cfg 222)
 bool resunit_w16_ok(int C, int d, int P);
-int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s2a, const float* s2b, int B,
+int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s2a, const float* s2b, int B, int P,
                        hipStream_t st);
 int resunit_launch(const float* x_raw, const float* x_act, const float* w7, const float* b7, const float* s2a,
                    const float* s2b, const float* w1, const float* b1, const float* osa, const float* osb,

@@ -533,7 +533,7 @@ extern __shared__ __attribute__((aligned(16))) unsigned char smem_xb[];
 
 template <int MT, int NT, int WM, int WN, int P, bool PW, int TPS, bool DB, bool B4, bool SWAP, int SIN, class Fin>
 __device__ __forceinline__ void conv1d_x6_body(const ConvArgs& a, Fin&& fin) {
-  static_assert(!SIN || (!PW && P == 3), "snake on load: x6 multi-tap launches only");
+  static_assert(!SIN || (!PW && P != 2), "snake on load: x6 / bf16 multi-tap launches only (h3 scales the raw chunk)");
   constexpr int BM = 16 * MT * WM;
   constexpr int BN = 16 * NT * WN;
   constexpr int QA = WM * MT;  // m-tiles per workgroup (1 KiB per plane each)
@@ -851,7 +851,8 @@ __device__ __forceinline__ void conv1d_x6_body(const ConvArgs& a, Fin&& fin) {
 #pragma unroll
           for (int j = 0; j < NT; ++j) {
             prefetch(j);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0);
+            acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][0], a0, acc[i][j], 0, 0, 0)
+                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[j][0], acc[i][j], 0, 0, 0);
           }
         } else {
           const frag_t a1 = af[sl][1];

@@ -52,10 +52,15 @@ __device__ __forceinline__ int w16_hs_off(int n, int g) { return n * 64 + 16 * (
 
 // SIN: 2 = snake on load with the coefficients staged in LDS (0 = the producer activated x)
 // B4: the 16-byte input staging (Tin % 4 == 0, 16-B aligned rows: every encoder shape); else single-float loads
+// P: 3 = x6 (three exact bf16 planes, six products; phase 1 one tap per K-step, as the x6 k7 launches), 1 = the bf16
+// precision mode of config 5 (one plane, one product; phase 1 four taps per K-step over two B buffers, as the bf16 k7
+// launches; h rounded to bf16 where the pointwise conv's staging rounded it)
 template <int P, int SIN, bool B4>
 __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvArgs e, RUW16Args r) {
-  static_assert(P == 3, "x6 operands");
+  static_assert(P == 3 || P == 1, "x6 or bf16 operands");
   typedef bf16x8_t frag_t;
+  constexpr int TPS1 = P == 3 ? 1 : 4;  // phase-1 taps per K-step
+  constexpr bool DB1 = P == 1;          // phase-1 double-buffered B tile
   {  // the per-channel coefficients into LDS by LDS-DMA (landed by the body's prologue vmcnt(0) + barrier):
      // [0] b7, [1] s2a, [2] s2b (bridge), [3] b1, [4] osa, [5] osb (epilogue; zeros when absent)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -70,7 +75,7 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
         reinterpret_cast<float*>(dst)[lane] = 0.f;
     }
   }
-  conv1d_x6_body<6, 2, 2, 8, P, false, 1, false, B4, false, SIN>(
+  conv1d_x6_body<6, 2, 2, 8, P, false, TPS1, DB1, B4, false, SIN>(
       a, [&](floatx4 (&acc)[6][2], int b, int m0, int n0, int wm, int wn, int lane, float) {
         (void)m0;
         unsigned char* Hs = smem_xb;  // aliases the phase-1 B tile and A buffers: every wave has passed the last
@@ -92,10 +97,14 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
                                       (f32x2){sb[0], sb[1]});
             const f32x2 hi = snake_pk((f32x2){acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]}, (f32x2){sa[2], sa[3]},
                                       (f32x2){sb[2], sb[3]});
+            unsigned char* dst = Hs + (co / X6_BKC) * (W16_HC * 64) + w16_hs_off(n, (co % X6_BKC) / 8) + (co % 8) * 2;
+            if constexpr (P == 1) {  // h rounded to bf16 (the pointwise conv's staging rounding)
+              *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){pk_bf16(lo.x, lo.y), pk_bf16(hi.x, hi.y)};
+              continue;
+            }
             unsigned h0, m0_, l0, h1, m1, l1;
             split2(lo.x, lo.y, h0, m0_, l0);
             split2(hi.x, hi.y, h1, m1, l1);
-            unsigned char* dst = Hs + (co / X6_BKC) * (W16_HC * 64) + w16_hs_off(n, (co % X6_BKC) / 8) + (co % 8) * 2;
             *reinterpret_cast<u32x2_t*>(dst) = (u32x2_t){h0, h1};
             *reinterpret_cast<u32x2_t*>(dst + W16_HPLANE) = (u32x2_t){m0_, m1};
             *reinterpret_cast<u32x2_t*>(dst + 2 * W16_HPLANE) = (u32x2_t){l0, l1};
@@ -104,10 +113,10 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
 
         // the k=1 conv over Hs: acc2[i][jj] = rows 48 mg + 16 i, local columns (2 ng + jj) * 16 ..
         const unsigned char* w1b = reinterpret_cast<const unsigned char*>(r.w1) + lane * 16;
-        auto wfrag = [&](int kc, int i, frag_t (&w)[3]) {
+        auto wfrag = [&](int kc, int i, frag_t (&w)[P]) {
 #pragma unroll
-          for (int p = 0; p < 3; ++p)
-            w[p] = *reinterpret_cast<const frag_t*>(w1b + ((kc * 3 + p) * W16_QA + mg * 3 + i) * 1024);
+          for (int p = 0; p < P; ++p)
+            w[p] = *reinterpret_cast<const frag_t*>(w1b + ((kc * P + p) * W16_QA + mg * 3 + i) * 1024);
         };
         auto phase2 = [&](floatx4 (&acc2)[3][2]) {
 #pragma unroll
@@ -116,30 +125,35 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
             for (int jj = 0; jj < 2; ++jj) acc2[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
           for (int kc = 0; kc < W16_NCK; ++kc) {
-            frag_t hf[2][3];
+            frag_t hf[2][P];
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) {
               const unsigned char* src = Hs + kc * (W16_HC * 64) + w16_hs_off((2 * ng + jj) * 16 + (lane & 15), lane >> 4);
 #pragma unroll
-              for (int p = 0; p < 3; ++p) hf[jj][p] = *reinterpret_cast<const frag_t*>(src + p * W16_HPLANE);
+              for (int p = 0; p < P; ++p) hf[jj][p] = *reinterpret_cast<const frag_t*>(src + p * W16_HPLANE);
             }
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
               // (loaded at the m-tile that uses it: a prefetch one m-tile ahead spilled 37 VGPRs; the other three
               // waves of the SIMD cover the L1 / L2 latency)
-              frag_t w[3];
+              frag_t w[P];
               if (BC_ABL(e.dbg, 2)) {
-                w[0] = hf[0][1], w[1] = hf[1][0], w[2] = hf[0][2];
+#pragma unroll
+                for (int p = 0; p < P; ++p) w[p] = hf[p & 1][0];
               } else {
                 wfrag(kc, i, w);
               }
               if (BC_ABL(e.dbg, 1)) {
-                acc2[i][0][0] += (float)w[0][0] + (float)w[1][1] + (float)w[2][2];
+                acc2[i][0][0] += (float)w[0][0] + (float)w[P - 1][1];
                 continue;
               }
 #pragma unroll
               for (int jj = 0; jj < 2; ++jj) {
                 floatx4 t = acc2[i][jj];
+                if constexpr (P == 1) {  // one bf16 product (h as A: the transposed tile of the shared epilogue)
+                  acc2[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[0], t, 0, 0, 0);
+                  continue;
+                }
                 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[2], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][1], w[1], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][2], w[0], t, 0, 0, 0);
@@ -263,19 +277,21 @@ static bool ru_w16_on() {
   return v;
 }
 
-static size_t w16_lds(int d) {
+static size_t w16_lds(int d, int P) {
   const X6Tile t{6, 2, 2, 8};
-  const size_t ph1 = x6_lds(t, x6_ncol(t, 7, 1, d), 3, 1);  // B tile + double-buffered A (one tap per K-step)
+  // B tile(s) + double-buffered A: x6 one tap per K-step, bf16 four taps over two B buffers (the k7 launches' variants)
+  const size_t ph1 = P == 3 ? x6_lds(t, x6_ncol(t, 7, 1, d), 3, 1) : x6_lds(t, x6_ncol(t, 7, 1, d), 1, 1, 4, 2);
   if (ph1 > (size_t)W16_COEF) return ~(size_t)0;             // the coefficients sit past phase 1's buffers
   return (size_t)W16_COEF + W16_LDS_EXTRA;
 }
 
 bool resunit_w16_ok(int C, int d, int P) {
-  return ru_w16_on() && P == 3 && C == W16_C && d >= 1 && d <= W16_MAXD && w16_lds(d) <= 160 * 1024;
+  return ru_w16_on() && (P == 3 || P == 1) && C == W16_C && d >= 1 && d <= W16_MAXD && w16_lds(d, P) <= 160 * 1024;
 }
 
-int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s2a, const float* s2b, int B,
+int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s2a, const float* s2b, int B, int P,
                        hipStream_t st) {
+  if (P != 3 && P != 1) return BC_ERR_ARG;
   if (a.Cin != W16_C || a.Cout != W16_C || a.K != 7 || a.s != 1 || a.d < 1 || a.d > W16_MAXD) return BC_ERR_UNSUPPORTED;
   const X6Tile t{6, 2, 2, 8};
   const int ncol = x6_ncol(t, 7, 1, a.d);
@@ -294,7 +310,7 @@ int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s
   if (nwg > 0x7fffffffLL) return BC_ERR_ARG;
   if ((long long)a.Cin * a.Tin * 4 > 0x7fffffffLL) return BC_ERR_UNSUPPORTED;
   a.nwg = (int)nwg;
-  const size_t lds = w16_lds(a.d);
+  const size_t lds = w16_lds(a.d, P);
   if (lds > 160 * 1024) return BC_ERR_UNSUPPORTED;
   RUW16Args r{w1, s2a, s2b};
   // BC_W16_DEBUG (BC_ABLATION builds only, wrong results, timing): 1 no phase-2 MFMAs, 2 no k=1 weight loads, 4 no
@@ -311,14 +327,21 @@ int resunit_w16_launch(ConvArgs& a, ConvArgs& e, const float* w1, const float* s
   a.dbg = dbg1;
   const bool b4 = x6_b4_on() && x6_b4_fits(a);
   a.sin_lds = W16_COEF + 6 * W16_C * 4;
-  if (a.isa && b4)
-    hipLaunchKernelGGL((resunit_w16_kernel<3, 2, true>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);
-  else if (a.isa)
-    hipLaunchKernelGGL((resunit_w16_kernel<3, 2, false>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);
-  else if (b4)
-    hipLaunchKernelGGL((resunit_w16_kernel<3, 0, true>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);
-  else
-    hipLaunchKernelGGL((resunit_w16_kernel<3, 0, false>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);
+#define BC_W16_LAUNCH(PP)                                                                                    \
+  if (a.isa && b4)                                                                                           \
+    hipLaunchKernelGGL((resunit_w16_kernel<PP, 2, true>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);        \
+  else if (a.isa)                                                                                            \
+    hipLaunchKernelGGL((resunit_w16_kernel<PP, 2, false>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);       \
+  else if (b4)                                                                                               \
+    hipLaunchKernelGGL((resunit_w16_kernel<PP, 0, true>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);        \
+  else                                                                                                       \
+    hipLaunchKernelGGL((resunit_w16_kernel<PP, 0, false>), dim3(a.nwg), dim3(1024), lds, st, a, e, r);
+  if (P == 3) {
+    BC_W16_LAUNCH(3)
+  } else {
+    BC_W16_LAUNCH(1)
+  }
+#undef BC_W16_LAUNCH
   BC_CHECK_LAUNCH();
   return BC_OK;
 }

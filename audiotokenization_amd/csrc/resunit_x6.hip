@@ -553,8 +553,8 @@ int resunit_select_cfg(int C, int d, int mode) {
   if (mode < 1 || mode > 3 || C < 16 || C % 16 || d <= 0) return -1;
   const int P = mode == 3 ? 2 : mode == 2 ? 1 : 3;
   const int forced = ru_forced_cfg();
-  // C = 192 (x6): the 16-wave 192 x 256 tile, k=1 weights streamed into registers (resunit_w16.hip)
-  if (!forced && resunit_w16_ok(C, d, P)) return 122;
+  // C = 192 (x6, bf16): the 16-wave 192 x 256 tile, k=1 weights streamed into registers (resunit_w16.hip)
+  if (!forced && resunit_w16_ok(C, d, P)) return P == 1 ? 222 : 122;
   for (int cfg : (P == 3 ? kRUCandidates : kRUCandidatesP12)) {
     const X6Tile& t = x6_tile(cfg);
     if (x6_BM(t) != C) continue;
@@ -624,9 +624,9 @@ static int launch_ru(ConvArgs& a, ConvArgs& e, RUExtra& r, int B, hipStream_t st
 int resunit_kernel_name(int cfg, int C, int d, char* buf, int n) {
   const int mode = cfg / 100;  // 1 x6, 2 bf16, 3 h3
   if (mode < 1 || mode > 3 || !resunit_cfg_ok(cfg, C, d)) return -1;
-  if (cfg == 122) {  // resunit_w16.hip; the encoder flow activates on load unless BIGCODEC_RU_SNAKE_IN=0 (blocks.py)
-    const char* e = getenv("BIGCODEC_RU_SNAKE_IN");
-    return snprintf(buf, n, "resunit_w16_kernel<3, %d, true>", e && atoi(e) == 0 ? 0 : 2);
+  if (cfg == 122 || cfg == 222) {  // resunit_w16.hip; the encoder flow activates on load unless BIGCODEC_RU_SNAKE_IN=0
+    const char* e = getenv("BIGCODEC_RU_SNAKE_IN");      // (blocks.py)
+    return snprintf(buf, n, "resunit_w16_kernel<%d, %d, true>", cfg == 122 ? 3 : 1, e && atoi(e) == 0 ? 0 : 2);
   }
   if (mode == 3 && resunit_rr_ok(C, d)) return resunit_rr_kernel_name(C, d, buf, n);
   const X6Tile& t = x6_tile(cfg);
@@ -660,11 +660,12 @@ int resunit_launch(const float* x_raw, const float* x_act, const float* w7, cons
   }();
   RUExtra r{w1, s2a, s2b, 0, 0, dbg, isa, isb};
   if (isa) a.x = x_raw;  // snake on load
-  if (cfg == 122) {
-    if (!resunit_w16_ok(C, d, 3)) return BC_ERR_UNSUPPORTED;
+  if (cfg == 122 || cfg == 222) {
+    const int P = cfg == 122 ? 3 : 1;
+    if (!resunit_w16_ok(C, d, P)) return BC_ERR_UNSUPPORTED;
     a.isa = isa;
     a.isb = isb;
-    return resunit_w16_launch(a, e, w1, s2a, s2b, B, st);
+    return resunit_w16_launch(a, e, w1, s2a, s2b, B, P, st);
   }
 #define BC_RU_CASES(ID, MT, NT, WM, WN)                           \
   case 100 + ID: return launch_ru<MT, NT, WM, WN, 3>(a, e, r, B, st); \

@@ -70,8 +70,10 @@ def kernel_peak(kname: str):
         planes = "3"
     if kname.startswith("pw_presplit_kernel"):  # the h3 pre-split GEMM
         planes = "2"
-    if kname.startswith(("conv1d_x6ra_kernel", "resunit_w16_kernel")):  # x6 (three bf16 planes) only
+    if kname.startswith("conv1d_x6ra_kernel"):  # x6 (three bf16 planes) only
         planes = "3"
+    if kname.startswith("resunit_w16_kernel") and targs:  # <P, SIN, B4>: x6 (3) or bf16 (1)
+        planes = targs[0]
     if kname.startswith(("resunit_rr_kernel", "resunit_strip_kernel")):  # resunit_rr.hip: h3 (two fp16 planes) only
         planes = "2"
     if planes == "1":

@@ -301,6 +301,7 @@ def test_kernel_names_come_from_the_launchers():
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(48, 3, 1), 48, 3) == "resunit_x6_kernel<3, 1, 1, 8, 3, 2>"
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(96, 3, 1), 96, 3) == "resunit_x6_kernel<6, 1, 1, 8, 3, 1>"
     assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(192, 3, 1), 192, 3).startswith("resunit_w16_kernel<3, ")
+    assert L.resunit_kernel_name(lib.bc_resunit_select_cfg(192, 3, 2), 192, 3).startswith("resunit_w16_kernel<1, ")
     for C in (16, 32):
         nx = L.resunit_kernel_name(lib.bc_resunit_select_cfg(C, 3, 1), C, 3)
         assert re.search(r", 3, 1>$", nx), nx

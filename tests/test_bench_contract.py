@@ -15,6 +15,7 @@ def test_kernel_peak_by_operand_planes():
         "resunit_strip_kernel<3>": h3,
         "resunit_x6_kernel<3, 1, 1, 8, 3, 2>": x6,
         "resunit_w16_kernel<3, 2, true>": x6,
+        "resunit_w16_kernel<1, 2, true>": bf16,
         "lstm_seq2_x6_kernel<12, 3, 2>": x6,
         "lstm_seq2_x6_kernel<12, 2, 1>": h3,
         "pw_presplit_x6_kernel": x6,

@@ -547,12 +547,14 @@ def test_resunit_w16_c192(dev, d, causal, B, T):
 
 
 @pytest.mark.parametrize("C,d,causal,B,T", [(48, 1, False, 2, 1001), (48, 9, True, 1, 24000), (96, 3, False, 2, 513),
-                                           (96, 9, False, 1, 4096), (64, 1, True, 2, 300), (16, 3, False, 3, 257)])
+                                           (96, 9, False, 1, 4096), (64, 1, True, 2, 300), (16, 3, False, 3, 257),
+                                           (192, 1, False, 2, 1001), (192, 9, True, 1, 24000), (192, 3, False, 2, 130)])
 def test_resunit_fused_bf16(dev, C, d, causal, B, T):
     """Precision 'bf16' (config 5) runs the ResidualUnit in one launch too (resunit_x6_kernel<..., P = 1>):
     the k=7 input and the activated h rounded to bf16 as the lone bf16 convs round their inputs, fp32
     accumulation.  Against the two-launch bf16 path: the same roundings and the same accumulation
-    order, so agreement to a few fp32 ulps; against the fp32 oracle: bf16-rounding sized."""
+    order, so agreement to a few fp32 ulps; against the fp32 oracle: bf16-rounding sized.  C = 192 runs the
+    16-wave unit (resunit_w16_kernel<1, ...>: phase 1 four taps per K-step, h rounded to bf16 in LDS)."""
     from audiotokenization_amd.blocks import produce_conv
 
     old = L.precision_mode()
@@ -570,7 +572,11 @@ def test_resunit_fused_bf16(dev, C, d, causal, B, T):
         ru.to(dev)
         cfg = ru._fused_cfg()
         assert 200 <= cfg < 300, cfg
-        assert "resunit_x6_kernel" in L.resunit_kernel_name(cfg, C, d) and ", 1, " in L.resunit_kernel_name(cfg, C, d)
+        name = L.resunit_kernel_name(cfg, C, d)
+        if C == 192:
+            assert cfg == 222 and name.startswith("resunit_w16_kernel<1, "), (cfg, name)
+        else:
+            assert "resunit_x6_kernel" in name and ", 1, " in name, name
         xd = x.to(dev)
         xa = ru.first_act(xd)
         got = ru.flow(xd, xa)[0].cpu()
