@@ -156,6 +156,11 @@ int bc_conv1d_fwd(const float* x, const float* w_packed, const float* bias, cons
   a.Cin = Cin; a.Tin = Tin; a.Cout = Cout; a.Nout = Tout;
   a.K = K; a.s = stride; a.d = dilation; a.pl = pad_left;
   a.yT = Tout; a.ostride = 1; a.ooff = 0; a.epi = epilogue;
+#ifdef BC_ABLATION
+  // BC_ABL_PW_RAW_ONLY=1 (ablation builds, wrong results, timing): dual-output pointwise convs write the raw output only
+  static const bool raw_only = getenv("BC_ABL_PW_RAW_ONLY") != nullptr;
+  if (raw_only && K == 1 && y2) a.y2 = nullptr, a.osa = nullptr, a.osb = nullptr;
+#endif
   return conv_launch(a, B, cfg, S(stream));
 }
 

@@ -22,7 +22,7 @@ struct ConvArgs {
   int ps;              // 0: off
   int cin0;            // real input channels when ps != 0
   const float* wsc;    // h3 kernels: 1 / weight scale per output row (stored after the packed planes)
-  int dbg;             // BC_X6_DEBUG timing experiments (x6 kernel): 1 no A copies, 2 no B loads, 4 no B stores, 8 no epilogue, 16 s_setprio(1) around the MFMAs
+  int dbg;             // BC_X6_DEBUG timing experiments (x6 kernel): 1 no A copies, 2 no B loads, 4 no B stores, 8 no epilogue, 16 s_setprio(1) around the MFMAs, 32 no Snake on load (conv1d_x6_body)
   // filled by conv_launch
   int vec;             // 16-byte epilogue accesses allowed (conv_epilogue_vec_ok)
   int nchunks, win, bstage, astage;

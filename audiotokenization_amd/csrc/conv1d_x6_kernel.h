@@ -734,7 +734,7 @@ __device__ __forceinline__ void conv1d_x6_body(const ConvArgs& a, Fin&& fin) {
       const int col = bcol(i);
       if (col < ncol) {
         if constexpr (SIN) {
-          const f32x2 v = snake_pk((f32x2){w0[i], w1[i]}, sin_a, sin_b);
+          const f32x2 v = BC_ABL(a.dbg, 32) ? (f32x2){w0[i], w1[i]} : snake_pk((f32x2){w0[i], w1[i]}, sin_a, sin_b);
           put(col, bp, v.x, v.y, Bt, sc);
         } else {
           put(col, bp, w0[i], w1[i], Bt, sc);
@@ -750,7 +750,8 @@ __device__ __forceinline__ void conv1d_x6_body(const ConvArgs& a, Fin&& fin) {
       for (int j = 0; j < 4; ++j)
         if (col0 + j >= 0 && col0 + j < ncol) {
           if constexpr (SIN) {
-            const f32x2 v = snake_pk((f32x2){w0[it][j], w1[it][j]}, sin_a, sin_b);
+            const f32x2 v = BC_ABL(a.dbg, 32) ? (f32x2){w0[it][j], w1[it][j]}
+                                              : snake_pk((f32x2){w0[it][j], w1[it][j]}, sin_a, sin_b);
             put(col0 + j, p4, v.x, v.y, Bt, sc);
           } else {
             put(col0 + j, p4, w0[it][j], w1[it][j], Bt, sc);
