@@ -55,6 +55,9 @@ __device__ __forceinline__ int rr_bfull(int col, int g) { return col * 64 + 16 *
 // ds_read_b64 fragments of 16 consecutive columns hit 64 distinct banks
 __device__ __forceinline__ int rr_btail(int col, int h) { return col * 32 + 16 * (h ^ ((col >> 3) & 1)); }
 // h tile (phase-2 A operand): full chunk [BN][64 B] swizzled by (n >> 2) & 3, tail [BN][32 B]
+// (16-B groups XOR-swizzled by (n >> 2) & 3: the phase-2 fragment reads are 2-way conflicted, the bridge's 8-byte
+// writes 2-way under any 16-B swizzle; the conflict-free (n >> 1) & 3 halved the conflict cycles and changed no unit's
+// time, profiles/r06s_hs_swizzle_rejected.txt)
 __device__ __forceinline__ int rr_hfull(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
 // one k=7 tap of a full 32-channel chunk over NT n-tiles: B fragments from the input tile (2 planes at

@@ -48,6 +48,9 @@ constexpr int W16_COEF = 3 * W16_HPLANE;    // LDS: per-channel coefficients [6]
                                             // every phase-1 buffer (x6_lds <= 131.5 KiB at d <= 9) and Hs
 constexpr int W16_LDS_EXTRA = 8 * W16_C * 4;  // + [6] isa, [7] isb (snake on load, SIN 2)
 
+// (16-B groups XOR-swizzled by (n >> 2) & 3: the phase-2 fragment reads are 2-way conflicted, the bridge's 8-byte
+// writes 2-way under any 16-B swizzle; the conflict-free (n >> 1) & 3 halved the conflict cycles and changed no unit's
+// time, profiles/r06s_hs_swizzle_rejected.txt)
 __device__ __forceinline__ int w16_hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
 // SIN: 2 = snake on load with the coefficients staged in LDS (0 = the producer activated x)
@@ -151,15 +154,15 @@ __global__ void __launch_bounds__(1024, 1) resunit_w16_kernel(ConvArgs a, ConvAr
               for (int jj = 0; jj < 2; ++jj) {
                 floatx4 t = acc2[i][jj];
                 if constexpr (P == 1) {  // one bf16 product (h as A: the transposed tile of the shared epilogue)
-                  acc2[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[0], t, 0, 0, 0);
-                  continue;
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[0], t, 0, 0, 0);
+                } else {
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[2], t, 0, 0, 0);
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][1], w[1], t, 0, 0, 0);
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][2], w[0], t, 0, 0, 0);
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[1], t, 0, 0, 0);
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][1], w[0], t, 0, 0, 0);
+                  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[0], t, 0, 0, 0);
                 }
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[2], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][1], w[1], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][2], w[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[1], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][1], w[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[jj][0], w[0], t, 0, 0, 0);
                 acc2[i][jj] = t;
               }
             }

@@ -46,6 +46,9 @@ struct RUExtra {
   const float* isb;
 };
 
+// (16-B groups XOR-swizzled by (n >> 2) & 3: the phase-2 fragment reads are 2-way conflicted, the bridge's 8-byte
+// writes 2-way under any 16-B swizzle; the conflict-free (n >> 1) & 3 halved the conflict cycles and changed no unit's
+// time, profiles/r06s_hs_swizzle_rejected.txt)
 __device__ __forceinline__ int hs_off(int n, int g) { return n * 64 + 16 * (g ^ ((n >> 2) & 3)); }
 
 // Minimum waves per SIMD the unit is compiled for: 4 (<= 128 VGPRs, two workgroups per CU) for the NT = 1
