@@ -125,7 +125,14 @@ def all_gather_codes(codes: torch.Tensor, group=None) -> torch.Tensor:
 
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return codes.unsqueeze(0)
-    world = dist.get_world_size(group)
+    return _all_gather_wire(codes, dist.get_world_size(group), group)
+
+
+def _all_gather_wire(codes: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """The collective of all_gather_codes (also run at world 1 by tests/test_gpu_extract.py, so the RCCL call, the int16
+    byte view and the reassembly execute on a GPU): (Nq, B, F) per rank -> (W, Nq, B, F)."""
+    import torch.distributed as dist
+
     codes = codes.contiguous()
     # int16 (the on-disk type) travels as its bytes: RCCL and gloo have no 16-bit integer type
     wire = codes.view(torch.int8) if codes.dtype == torch.int16 else codes

@@ -36,3 +36,35 @@ def test_extract_sharded_world1_writes_per_clip_npy(dev, tmp_path):
         arr = np.load(path)
         assert arr.dtype == np.int16 and arr.shape == (T // 200, 1)
         np.testing.assert_array_equal(arr[:, 0], ref[c][0, 0].cpu().numpy().astype(np.int16))
+
+
+def test_rccl_codes_all_gather_world1(dev):
+    """The codes all-gather's collective (extract._all_gather_wire: the int16 byte view, dist.all_gather_into_tensor,
+    the reassembly) executed over RCCL on the GPU.  One GPU per box: a world-1 "nccl" group (all_gather_codes itself
+    returns early at world 1, so without this the RCCL call never ran on hardware); worlds 2-8 run the same function
+    over gloo in tests/test_distributed_gloo.py."""
+    import socket
+
+    import torch.distributed as dist
+
+    from audiotokenization_amd.extract import _all_gather_wire
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(dev))
+    try:
+        assert dist.get_backend() == "nccl"
+        g = torch.Generator().manual_seed(5)
+        for dtype in (torch.int16, torch.int64):
+            codes = torch.randint(-32768, 32767, (2, 7, 61), generator=g).to(dtype).to(dev)
+            out = _all_gather_wire(codes, 1)
+            torch.cuda.synchronize()
+            assert out.dtype == dtype and out.shape == (1, 2, 7, 61)
+            assert torch.equal(out[0].cpu(), codes.cpu())
+    finally:
+        dist.destroy_process_group()
